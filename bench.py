@@ -1,0 +1,257 @@
+"""Benchmark: matched-pattern events/s (BASELINE.json metric) on MI355X.
+
+Default workload = BASELINE.json configs[2] (config 3): keyed
+`partition with (k of A, k of B) begin from every s1=A[price > 0.5] ->
+s2=B[id % 7 == 0] within 10 sec select s1.k, s1.price, s2.price, s2.ts ...`,
+K = 2^20 partition keys, N = 2^28 events per step, R = 400 events/ms.
+A step = one pass of the hot path (predicate + key-bucket partition + per-key
+NFA walk + match emission) over one batch of N events already resident in
+HBM; the per-key pattern state carries from step to step (each step is the
+next N events of one stream).  With --gpus N > 1 (torchrun), each rank owns
+the keys k % N == rank and processes N events per step (weak scaling).
+
+`--workload filter` runs configs[1] (config 2): `inputStream[price > 0.5 and
+id % 7 == 0] select *` over 10^8 events.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "flink-siddhi_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+PATTERN_IN_BYTES = 4 + 8 + 1 + 4 + 8     # k, ts, stream, id, price per event
+PATTERN_OUT_BYTES = 4 + 8 + 8 + 8 + 8    # k, p1, p2, t + event ts per match
+FILTER_IN_BYTES = 4 + 8                   # id, price per event
+FILTER_OUT_BYTES = 4 + 4 + 8 + 8 + 8      # id, name, price, timestamp + event ts
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["pattern", "filter"], default="pattern")
+    ap.add_argument("--events", type=int, default=0, help="events per step per GPU")
+    ap.add_argument("--keys", type=int, default=1 << 20)
+    ap.add_argument("--rate", type=int, default=400, help="events per ms")
+    ap.add_argument("--chunk", type=int, default=1 << 22)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def dist_init(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(world, v: float) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(world, v: float) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline_pattern(args, budget_s):
+    """Oracle C restatement (kind "port"), single thread, bounded sample."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cep_oracle as CO
+    from flink_siddhi import workload
+    po = CO.PatternOracle(args.keys, CO.cond(("price", 0, ">", 0.5)),
+                          CO.cond(("id", 7, "==", 0)), every=True, within=10000)
+    chunk = 1 << 22
+    done = 0
+    spent = 0.0
+    matches = 0
+    while spent < budget_s and done < (1 << 28):
+        w = workload.generate(done, chunk, args.keys, rate=args.rate)
+        t0 = time.perf_counter()
+        _, _, m = po.run(w, out_cap=chunk)
+        spent += time.perf_counter() - t0
+        matches += m
+        done += chunk
+    return {"value": done / spent, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "first %d events of the config-3 stream (K=%d, R=%d/ms), "
+                      "oracle/cep_oracle.c single-threaded, %d matches, %.1f s"
+                      % (done, args.keys, args.rate, matches, spent)}
+
+
+def cpu_baseline_filter(args, n_total, budget_s):
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cep_oracle as CO
+    from flink_siddhi import workload
+    f = CO.cond(("price", 0, ">", 0.5), ("id", 7, "==", 0))
+    chunk = 1 << 23
+    done, spent = 0, 0.0
+    while spent < budget_s and done < n_total:
+        w = workload.generate(done, chunk, 1, single_stream=True)
+        t0 = time.perf_counter()
+        CO.filter_indices(w["id"], w["price"], f)
+        spent += time.perf_counter() - t0
+        done += chunk
+    return {"value": done / spent, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "first %d events of the config-2 stream, oracle/cep_oracle.c "
+                      "single-threaded, %.1f s" % (done, spent)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import flink_siddhi as fs
+    from flink_siddhi import _lib as L
+    from flink_siddhi import workload
+
+    world, rank, local = dist_init(args)
+    pattern = args.workload == "pattern"
+    n = args.events or ((1 << 28) if pattern else 100_000_000)
+    steps, warm = args.steps, args.warmup
+
+    if pattern:
+        plan = workload.PATTERN_PLAN
+        opts = dict(device=local, key_capacity=(args.keys + world - 1) // world,
+                    key_stride=world, key_offset=rank, chunk_events=args.chunk,
+                    profile=1, ordered_output=0)
+    else:
+        plan = workload.FILTER_PLAN
+        opts = dict(device=local, profile=1, ordered_output=0)
+    rt = fs.SiddhiAppRuntime(plan, **opts)
+
+    # Inputs for every step, generated on the device before the timed region.
+    # Multi-GPU: rank r's events are the ones whose key it owns (the result of
+    # the keyBy shuffle), drawn from its own contiguous index ranges.
+    batches = []
+    for s in range(warm + steps):
+        first = (s * world + rank) * n
+        d = workload.generate_device(first, n, args.keys, rate=args.rate,
+                                     single_stream=not pattern, device="cuda")
+        if pattern and world > 1:
+            d["k"] = (d["k"] // world) * world + rank     # owned keys, same distribution
+        if not pattern:
+            d["name"] = torch.zeros(n, dtype=torch.int32, device="cuda")
+        batches.append(d)
+    torch.cuda.synchronize()
+
+    def step(d):
+        if pattern:
+            rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
+        else:
+            rt.send("inputStream", d["ts"], [d["id"], d["name"], d["price"], d["ts"]])
+        rt.flush()
+
+    for s in range(warm):
+        step(batches[s])
+    st0 = rt.stats()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step(batches[warm + s])
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    st1 = rt.stats()
+    dt_max = max_over_ranks(world, dt)
+    events_total = sum_over_ranks(world, float(n * steps))
+    matches_total = sum_over_ranks(world, float(st1.matches_out - st0.matches_out))
+    value = events_total / dt_max
+
+    # per-kernel HIP-event times on the engine's stream over the timed region
+    kern = {}
+    for k, name in ((L.K_PARTITION, "k_partition"), (L.K_WALK, "k_walk"), (L.K_FILTER, "k_filter")):
+        launches = st1.kernel_launches[k] - st0.kernel_launches[k]
+        ms = st1.kernel_ms[k] - st0.kernel_ms[k]
+        if launches:
+            kern[name] = {"launches": int(launches), "avg_us": 1e3 * ms / launches,
+                          "total_ms": ms}
+    dom = max(kern, key=lambda k: kern[k]["total_ms"])
+    m_per_event = (st1.matches_out - st0.matches_out) / float(n * steps)
+    if pattern:
+        chunk_events = min(args.chunk, n)
+        per_launch = {"k_partition": PATTERN_IN_BYTES * chunk_events,
+                      "k_walk": PATTERN_OUT_BYTES * m_per_event * chunk_events}
+        alg_per_event = PATTERN_IN_BYTES + PATTERN_OUT_BYTES * m_per_event
+    else:
+        per_launch = {"k_filter": (FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event) * n}
+        alg_per_event = FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event
+    achieved = per_launch[dom] / (kern[dom]["avg_us"] * 1e-6) / 1e9
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "bytes_per_launch": per_launch[dom], "avg_launch_us": round(kern[dom]["avg_us"], 2)}
+    per_gpu_events = value / world
+    pipeline = {"alg_bytes_per_event": round(alg_per_event, 3),
+                "achieved": round(per_gpu_events * alg_per_event / 1e9, 1), "unit": "GB/s",
+                "frac": round(per_gpu_events * alg_per_event / 1e9 / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline_pattern(args, args.cpu_seconds) if pattern else \
+            cpu_baseline_filter(args, n, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "matched-pattern events/sec (whole node) at 1/2/4/8 MI355X + % HBM roofline",
+            "value": round(value, 1), "unit": "events/s", "n_gpus": world,
+            "steps": steps, "warmup": warm, "ms_per_step": round(1e3 * dt_max / steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64+int32+int64", "data": "synthetic (splitmix64 counter stream, BASELINE.md §3)",
+            "config": ({"workload": "config3: keyed every A -> B within 10 sec, partition with k",
+                        "keys": args.keys, "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
+                        "chunk_events": args.chunk, "parallelism": "key-sharded x%d" % world}
+                       if pattern else
+                       {"workload": "config2: inputStream[price > 0.5 and id % 7 == 0] select *",
+                        "events_per_step_per_gpu": n, "parallelism": "replicas x%d" % world}),
+            "matches_per_s": round(matches_total / dt_max, 1),
+            "matches_per_event": round(m_per_event, 5),
+            "roofline": roofline,
+            "pipeline_roofline": pipeline,
+            "kernels": kern,
+            "cpu_baseline": cpu,
+            "speedup_vs_cpu_baseline": round(value / cpu["value"], 1) if cpu else None,
+        }
+        print(json.dumps(out), flush=True)
+    rt.shutdown()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

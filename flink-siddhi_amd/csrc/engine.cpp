@@ -1,0 +1,886 @@
+// libcep runtime: the C ABI of include/cep.h over the gfx950 kernels.
+//
+// One cep_app = one Siddhi app runtime (AbstractSiddhiOperator.java:114-176
+// QueryRuntimeHandler).  Device layout (HBM, sized for 288 GB/GPU):
+//   * plan: VM instruction array + constant pool (tiny, read-only),
+//   * per output stream: typed columns + ts + seq + a device row cursor,
+//     capacity = the host-known bound on rows since the last flush (no
+//     device->host sync is ever needed to size a launch),
+//   * per keyed pattern: dense per-key state [key][S][2+ncap] words plus a
+//     pending count and `started` byte per key, and a chunk-sized record
+//     arena [tiles][2048 rows][rec_words] + tile offset table.
+// All work for a batch is enqueued on the app's HIP stream; cep_flush
+// synchronises, checks the device error word and delivers rows to callbacks.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cep.h"
+#include "frontend.h"
+#include "kernels.h"
+
+using namespace cep;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+bool dev_ensure(DevBuf* b, size_t bytes, hipStream_t s, bool keep) {
+  if (b->bytes >= bytes && b->p) return true;
+  size_t nb = std::max(bytes, b->bytes * 2);
+  void* p = nullptr;
+  if (hipMalloc(&p, nb) != hipSuccess) return false;
+  if (keep && b->p && b->bytes) hipMemcpyAsync(p, b->p, b->bytes, hipMemcpyDeviceToDevice, s);
+  if (b->p) {
+    hipStreamSynchronize(s);
+    hipFree(b->p);
+  }
+  b->p = p;
+  b->bytes = nb;
+  return true;
+}
+
+void dev_free(DevBuf* b) {
+  if (b->p) hipFree(b->p);
+  b->p = nullptr;
+  b->bytes = 0;
+}
+
+struct OutStream {
+  std::string id;
+  std::vector<int> types;
+  std::vector<DevBuf> cols;
+  DevBuf ts, seq;
+  unsigned long long* count = nullptr;   // device cursor
+  int64_t cap = 0;                       // allocated rows
+  int64_t bound = 0;                     // upper bound of rows since last flush
+  cep_emit_fn fn = nullptr;
+  void* user = nullptr;
+  // host copies for callback delivery
+  std::vector<std::vector<uint8_t>> hcols;
+  std::vector<int64_t> hts, hseq;
+};
+
+struct PatternRT {
+  int q = -1;
+  PatternArgs pa{};
+  DevBuf pcnt, started, slots;
+  DevBuf recs, tile_off;
+  int64_t chunk = 0;
+  int64_t extra_bound = 0;   // pending partials that may still complete
+};
+
+struct TimedLaunch {
+  int kind;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct cep_app {
+  CompiledApp app;
+  cep_options opt{};
+  hipStream_t stream = nullptr;
+  bool enabled = true;
+  std::string last_error;
+  std::vector<std::string> dict;
+  std::unordered_map<std::string, int32_t> dict_index;
+  DevBuf code, konst;
+  std::vector<OutStream> outs;
+  std::vector<PatternRT> pats;
+  DevBuf tile_state, ticket, err;
+  std::vector<DevBuf> stage;   // host-batch staging columns (+ts, +stream)
+  int64_t events_in = 0, matches_out = 0, batches = 0;
+  int64_t last_ts = INT64_MIN;
+  int64_t launches[8] = {0};
+  double kernel_ms[8] = {0};
+  std::vector<TimedLaunch> timed;
+  std::vector<hipEvent_t> event_pool;
+  std::vector<std::unique_ptr<char[]>> name_store;
+};
+
+namespace {
+
+void set_err(char* err, size_t errlen, const std::string& m) {
+  if (err && errlen) {
+    std::snprintf(err, errlen, "%s", m.c_str());
+  }
+}
+
+int fail(cep_app* a, int code, const std::string& m) {
+  if (a) a->last_error = m;
+  return code;
+}
+
+hipEvent_t pool_event(cep_app* a) {
+  if (!a->event_pool.empty()) {
+    hipEvent_t e = a->event_pool.back();
+    a->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct LaunchTimer {
+  cep_app* a;
+  int kind;
+  hipEvent_t s = nullptr;
+  LaunchTimer(cep_app* app, int k) : a(app), kind(k) {
+    a->launches[k]++;
+    if (a->opt.profile) {
+      s = pool_event(a);
+      hipEventRecord(s, a->stream);
+    }
+  }
+  ~LaunchTimer() {
+    if (a->opt.profile) {
+      hipEvent_t e = pool_event(a);
+      hipEventRecord(e, a->stream);
+      a->timed.push_back({kind, s, e});
+    }
+  }
+};
+
+void harvest_timers(cep_app* a) {
+  for (auto& t : a->timed) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, t.a, t.b);
+    a->kernel_ms[t.kind] += ms;
+    a->event_pool.push_back(t.a);
+    a->event_pool.push_back(t.b);
+  }
+  a->timed.clear();
+}
+
+int ensure_out_cap(cep_app* a, OutStream& o, int64_t need) {
+  if (need <= o.cap) return CEP_OK;
+  int64_t nc = std::max<int64_t>(need, std::max<int64_t>(o.cap * 2, 1 << 16));
+  for (size_t c = 0; c < o.cols.size(); ++c)
+    if (!dev_ensure(&o.cols[c], (size_t)nc * type_width(o.types[c]), a->stream, true))
+      return fail(a, CEP_E_DEVICE, "out of device memory (output columns)");
+  if (!dev_ensure(&o.ts, (size_t)nc * 8, a->stream, true) ||
+      !dev_ensure(&o.seq, (size_t)nc * 8, a->stream, true))
+    return fail(a, CEP_E_DEVICE, "out of device memory (output ts/seq)");
+  o.cap = nc;
+  return CEP_OK;
+}
+
+OutArgs out_args(OutStream& o, const Query& q) {
+  OutArgs oa{};
+  oa.ncols = (int32_t)o.cols.size();
+  for (int c = 0; c < oa.ncols; ++c) {
+    oa.col[c] = o.cols[c].p;
+    oa.type[c] = o.types[c];
+    oa.prog[c] = q.select[c].prog.off;
+  }
+  oa.ts = (int64_t*)o.ts.p;
+  oa.seq = (int64_t*)o.seq.p;
+  oa.count = o.count;
+  oa.cap = o.cap;
+  return oa;
+}
+
+int create_runtime(cep_app* a) {
+  const CompiledApp& app = a->app;
+  if (hipSetDevice(a->opt.device) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "no HIP device " + std::to_string(a->opt.device));
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, a->opt.device) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "hipGetDeviceProperties failed");
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    return fail(a, CEP_E_DEVICE, std::string("libcep is built for gfx950, device is ") +
+                                     prop.gcnArchName);
+  if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
+  size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
+  size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
+  if (!dev_ensure(&a->code, cb, a->stream, false) || !dev_ensure(&a->konst, kb, a->stream, false) ||
+      !dev_ensure(&a->err, 64, a->stream, false) || !dev_ensure(&a->ticket, 64, a->stream, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory (plan)");
+  if (!app.code.empty())
+    hipMemcpy(a->code.p, app.code.data(), app.code.size() * sizeof(Ins), hipMemcpyHostToDevice);
+  if (!app.konst.empty())
+    hipMemcpy(a->konst.p, app.konst.data(), app.konst.size() * 8, hipMemcpyHostToDevice);
+  hipMemset(a->err.p, 0, 64);
+  for (auto& sd : app.outputs) {
+    OutStream o;
+    o.id = sd.id;
+    for (auto& at : sd.attrs) o.types.push_back(at.type);
+    o.cols.resize(sd.attrs.size());
+    if (hipMalloc(&o.count, sizeof(unsigned long long)) != hipSuccess)
+      return fail(a, CEP_E_DEVICE, "out of device memory");
+    hipMemset(o.count, 0, sizeof(unsigned long long));
+    a->outs.push_back(std::move(o));
+  }
+  const int S = a->opt.pending_slots;
+  for (size_t qi = 0; qi < app.queries.size(); ++qi) {
+    const Query& q = app.queries[qi];
+    if (q.kind == Q_AGG)
+      return fail(a, CEP_E_UNSUPPORTED, "group-by aggregation is not yet on the device engine");
+    if (q.kind != Q_PATTERN) continue;
+    PatternRT rt;
+    rt.q = (int)qi;
+    PatternArgs& p = rt.pa;
+    p.a_stream = q.a_stream;
+    p.b_stream = q.b_stream;
+    p.f_prog = q.f.off;
+    p.g_raw_prog = q.g_raw.off;
+    p.g_walk_prog = q.g_walk.off;
+    p.every = q.every ? 1 : 0;
+    p.within = q.within;
+    p.key_col_a = q.key_col_a;
+    p.key_col_b = q.key_col_b;
+    p.nrec_a = (int)q.rec_cols_a.size();
+    p.nrec_b = (int)q.rec_cols_b.size();
+    for (int i = 0; i < p.nrec_a; ++i) p.rec_a[i] = q.rec_cols_a[i];
+    for (int i = 0; i < p.nrec_b; ++i) p.rec_b[i] = q.rec_cols_b[i];
+    p.ncap = (int)q.cap_from_rec.size();
+    for (int i = 0; i < p.ncap; ++i) p.cap_from_rec[i] = q.cap_from_rec[i];
+    p.rec_words = 3 + std::max(p.nrec_a, p.nrec_b);
+    p.slot_words = 2 + p.ncap;
+    p.pending_slots = S;
+    const bool keyed = q.key_col_a >= 0;
+    int64_t kcap = keyed ? a->opt.key_capacity : 1;
+    p.key_capacity = kcap;
+    p.key_stride = keyed ? std::max(1, a->opt.key_stride) : 1;
+    p.key_offset = keyed ? a->opt.key_offset : 0;
+    if (!keyed && (a->opt.key_stride > 1))
+      return fail(a, CEP_E_UNSUPPORTED, "an unpartitioned pattern cannot be sharded");
+    int lg = std::max(0, std::min(12, a->opt.buckets_log2));
+    while ((kcap >> lg) > kWalkMaxKeys && lg < 12) ++lg;
+    if ((kcap + (1 << lg) - 1) >> lg > kWalkMaxKeys)
+      return fail(a, CEP_E_CAPACITY, "key_capacity exceeds 1024 * 4096 keys");
+    if (!keyed) lg = 0;
+    p.buckets_log2 = lg;
+    const int64_t kc = kcap;
+    if (!dev_ensure(&rt.pcnt, (size_t)kc, a->stream, false) ||
+        !dev_ensure(&rt.started, (size_t)kc, a->stream, false) ||
+        !dev_ensure(&rt.slots, (size_t)kc * S * p.slot_words * 8, a->stream, false))
+      return fail(a, CEP_E_DEVICE, "out of device memory (pattern state)");
+    hipMemset(rt.pcnt.p, 0, (size_t)kc);
+    hipMemset(rt.started.p, 0, (size_t)kc);
+    int64_t chunk = a->opt.chunk_events;
+    chunk = std::max<int64_t>(chunk, kPartThreads * kPartItems);
+    chunk = std::min<int64_t>(chunk, (int64_t)kWalkMaxTiles * kPartThreads * kPartItems);
+    chunk = (chunk / (kPartThreads * kPartItems)) * (kPartThreads * kPartItems);
+    rt.chunk = chunk;
+    const int64_t ntiles = chunk / (kPartThreads * kPartItems);
+    if (!dev_ensure(&rt.recs, (size_t)chunk * p.rec_words * 8, a->stream, false) ||
+        !dev_ensure(&rt.tile_off, (size_t)ntiles * ((1 << lg) + 1) * 2, a->stream, false))
+      return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
+    rt.extra_bound = (int64_t)S * kc;
+    a->pats.push_back(rt);
+  }
+  hipStreamSynchronize(a->stream);
+  return CEP_OK;
+}
+
+const StreamSchema* find_schema(cep_app* a, const char* id) {
+  if (!id) return nullptr;
+  int i = a->app.input_index(id);
+  if (i >= 0) return &a->app.inputs[i];
+  i = a->app.output_index(id);
+  if (i >= 0) return &a->app.outputs[i];
+  return nullptr;
+}
+
+int fill_attrs(const StreamSchema* s, cep_attr* out, int cap, int* n) {
+  if (n) *n = (int)s->attrs.size();
+  for (int i = 0; i < (int)s->attrs.size() && i < cap; ++i) {
+    std::snprintf(out[i].name, sizeof(out[i].name), "%s", s->attrs[i].name.c_str());
+    out[i].type = s->attrs[i].type;
+  }
+  return CEP_OK;
+}
+
+// Run one filter query over a device batch.
+int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
+  OutStream& o = a->outs[a->app.output_index(q.out_stream)];
+  o.bound += rows.n;
+  int rc = ensure_out_cap(a, o, o.bound);
+  if (rc) return rc;
+  constexpr int64_t kTile = kFilterThreads * kFilterItems;
+  const int64_t ntiles = (rows.n + kTile - 1) / kTile;
+  if (ntiles == 0) return CEP_OK;
+  if (!dev_ensure(&a->tile_state, (size_t)ntiles * 8, a->stream, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory (tile state)");
+  hipMemsetAsync(a->tile_state.p, 0, (size_t)ntiles * 8, a->stream);
+  hipMemsetAsync(a->ticket.p, 0, 16, a->stream);
+  FilterArgs fa{};
+  fa.rows = rows;
+  fa.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
+  fa.in_stream = q.in_stream;
+  fa.filter_prog = q.filter.off;
+  fa.out = out_args(o, q);
+  fa.tile_state = (unsigned long long*)a->tile_state.p;
+  fa.ticket = (unsigned int*)a->ticket.p;
+  fa.err = (unsigned int*)a->err.p;
+  LaunchTimer t(a, CEP_K_FILTER);
+  launch_filter(fa, ntiles, a->stream);
+  return CEP_OK;
+}
+
+int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
+  const Query& q = a->app.queries[rt.q];
+  OutStream& o = a->outs[a->app.output_index(q.out_stream)];
+  if (o.bound == 0) o.bound = rt.extra_bound;
+  o.bound += rows_all.n;
+  int rc = ensure_out_cap(a, o, o.bound);
+  if (rc) return rc;
+  const int P = 1 << rt.pa.buckets_log2;
+  for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.chunk) {
+    RowsArgs rows = rows_all;
+    rows.row0 = rows_all.row0 + r0;
+    rows.n = std::min<int64_t>(rt.chunk, rows_all.n - r0);
+    if (r0 > 0) rows.prev_ts = INT64_MIN;   // checked inside the kernel via ts[row-1]
+    const int64_t ntiles = (rows.n + kPartThreads * kPartItems - 1) / (kPartThreads * kPartItems);
+    PartArgs pa{};
+    pa.rows = rows;
+    if (r0 > 0) pa.rows.prev_ts = INT64_MIN;
+    pa.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
+    pa.pat = rt.pa;
+    pa.tile_rows = kPartThreads * kPartItems;
+    pa.recs = (uint64_t*)rt.recs.p;
+    pa.tile_off = (uint16_t*)rt.tile_off.p;
+    pa.err = (unsigned int*)a->err.p;
+    {
+      LaunchTimer t(a, CEP_K_PARTITION);
+      launch_partition(pa, ntiles, a->stream);
+    }
+    WalkArgs wa{};
+    wa.vm = pa.vm;
+    wa.pat = rt.pa;
+    wa.recs = pa.recs;
+    wa.tile_off = pa.tile_off;
+    wa.ntiles = (int)ntiles;
+    wa.tile_rows = pa.tile_rows;
+    wa.seq_chunk0 = rows.seq0 + rows.row0;
+    wa.pcnt = (uint8_t*)rt.pcnt.p;
+    wa.started = (uint8_t*)rt.started.p;
+    wa.slots = (uint64_t*)rt.slots.p;
+    wa.out = out_args(o, q);
+    wa.err = pa.err;
+    {
+      LaunchTimer t(a, CEP_K_WALK);
+      launch_walk(wa, P, a->stream);
+    }
+  }
+  return CEP_OK;
+}
+
+int send_device_rows(cep_app* a, const RowsArgs& rows) {
+  for (size_t qi = 0; qi < a->app.queries.size(); ++qi) {
+    const Query& q = a->app.queries[qi];
+    int rc = CEP_OK;
+    if (q.kind == Q_FILTER) {
+      rc = run_filter(a, q, rows);
+    } else if (q.kind == Q_PATTERN) {
+      for (auto& rt : a->pats)
+        if (rt.q == (int)qi) rc = run_pattern(a, rt, rows);
+    }
+    if (rc) return rc;
+  }
+  return CEP_OK;
+}
+
+int check_device_error(cep_app* a) {
+  unsigned int e = 0;
+  hipMemcpy(&e, a->err.p, sizeof(e), hipMemcpyDeviceToHost);
+  if (!e) return CEP_OK;
+  hipMemset(a->err.p, 0, 64);
+  if (e & ERR_ORDER)   // root cause first: out-of-order input also defeats `within` pruning
+    return fail(a, CEP_E_ARG, "events not in event-time order: `within` requires non-decreasing timestamps");
+  if (e & ERR_PENDING)
+    return fail(a, CEP_E_CAPACITY, "per-key pending partial capacity exceeded (raise pending_slots)");
+  if (e & ERR_KEY_RANGE)
+    return fail(a, CEP_E_CAPACITY, "partition key outside [0, key_capacity) or not owned by this shard");
+  if (e & ERR_OUT_CAP) return fail(a, CEP_E_DEVICE, "output capacity exceeded");
+  return fail(a, CEP_E_DEVICE, "device error flags " + std::to_string(e));
+}
+
+}  // namespace
+
+// ======================================================================= C ABI
+extern "C" {
+
+void cep_default_options(cep_options* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->device = 0;
+  o->pending_slots = 16;
+  o->key_capacity = 1 << 20;
+  o->chunk_events = 1 << 22;
+  o->buckets_log2 = 10;
+  o->profile = 0;
+  o->ordered_output = 1;
+  o->key_stride = 1;
+  o->key_offset = 0;
+}
+
+int cep_validate(const char* plan, char* err, size_t errlen) {
+  if (!plan) {
+    set_err(err, errlen, "plan is null");
+    return CEP_E_ARG;
+  }
+  CompiledApp app;
+  std::string m;
+  int rc = compile_app(plan, &app, &m);
+  if (rc) set_err(err, errlen, m);
+  else set_err(err, errlen, "");
+  return rc;
+}
+
+int cep_plan_schema(const char* plan, const char* stream_id, cep_attr* out, int cap, int* n,
+                    char* err, size_t errlen) {
+  if (!plan || !stream_id) {
+    set_err(err, errlen, "null argument");
+    return CEP_E_ARG;
+  }
+  CompiledApp app;
+  std::string m;
+  int rc = compile_app(plan, &app, &m);
+  if (rc) {
+    set_err(err, errlen, m);
+    return rc;
+  }
+  const StreamSchema* s = nullptr;
+  int i = app.input_index(stream_id);
+  if (i >= 0) s = &app.inputs[i];
+  i = app.output_index(stream_id);
+  if (!s && i >= 0) s = &app.outputs[i];
+  if (!s) {
+    set_err(err, errlen, std::string("Unknown stream id ") + stream_id);
+    return CEP_E_UNDEFINED_STREAM;
+  }
+  return fill_attrs(s, out, cap, n);
+}
+
+cep_app* cep_create(const char* plan, const cep_options* opt, char* err, size_t errlen) {
+  if (!plan) {
+    set_err(err, errlen, "plan is null");
+    return nullptr;
+  }
+  auto* a = new cep_app();
+  if (opt) a->opt = *opt;
+  else cep_default_options(&a->opt);
+  if (a->opt.pending_slots <= 0 || a->opt.pending_slots > kMaxPending) {
+    set_err(err, errlen, "pending_slots must be in [1, " + std::to_string(kMaxPending) + "]");
+    delete a;
+    return nullptr;
+  }
+  if (a->opt.key_stride <= 0) a->opt.key_stride = 1;
+  std::string m;
+  int rc = compile_app(plan, &a->app, &m);
+  if (rc) {
+    set_err(err, errlen, m);
+    delete a;
+    return nullptr;
+  }
+  for (auto& s : a->app.strings) cep_dict_intern(a, s.c_str());
+  rc = create_runtime(a);
+  if (rc) {
+    set_err(err, errlen, a->last_error);
+    cep_destroy(a);
+    return nullptr;
+  }
+  set_err(err, errlen, "");
+  return a;
+}
+
+void cep_destroy(cep_app* a) {
+  if (!a) return;
+  if (a->stream) hipStreamSynchronize(a->stream);
+  harvest_timers(a);
+  for (auto e : a->event_pool) hipEventDestroy(e);
+  for (auto& o : a->outs) {
+    for (auto& c : o.cols) dev_free(&c);
+    dev_free(&o.ts);
+    dev_free(&o.seq);
+    if (o.count) hipFree(o.count);
+  }
+  for (auto& p : a->pats) {
+    dev_free(&p.pcnt);
+    dev_free(&p.started);
+    dev_free(&p.slots);
+    dev_free(&p.recs);
+    dev_free(&p.tile_off);
+  }
+  for (auto& s : a->stage) dev_free(&s);
+  dev_free(&a->code);
+  dev_free(&a->konst);
+  dev_free(&a->tile_state);
+  dev_free(&a->ticket);
+  dev_free(&a->err);
+  if (a->stream) hipStreamDestroy(a->stream);
+  delete a;
+}
+
+int cep_stream_schema(cep_app* a, const char* stream_id, cep_attr* out, int cap, int* n) {
+  if (!a) return CEP_E_ARG;
+  const StreamSchema* s = find_schema(a, stream_id);
+  if (!s) return fail(a, CEP_E_UNDEFINED_STREAM, std::string("Stream ") + (stream_id ? stream_id : "(null)") + " not defined");
+  return fill_attrs(s, out, cap, n);
+}
+
+int cep_input(cep_app* a, const char* stream_id) {
+  if (!a || !stream_id) return -CEP_E_ARG;
+  int i = a->app.input_index(stream_id);
+  if (i < 0) {
+    fail(a, CEP_E_UNDEFINED_STREAM, std::string("Stream ") + stream_id + " not defined");
+    return -CEP_E_UNDEFINED_STREAM;
+  }
+  return i;
+}
+
+int cep_set_callback(cep_app* a, const char* out_id, cep_emit_fn fn, void* user) {
+  if (!a || !out_id) return CEP_E_ARG;
+  int i = a->app.output_index(out_id);
+  if (i < 0) return fail(a, CEP_E_UNDEFINED_STREAM, std::string("Stream ") + out_id + " not defined");
+  a->outs[i].fn = fn;
+  a->outs[i].user = user;
+  return CEP_OK;
+}
+
+int cep_send_batch(cep_app* a, const cep_batch* b) {
+  if (!a || !b) return CEP_E_ARG;
+  if (!a->enabled) return CEP_OK;   // AbstractSiddhiOperator.java:128
+  if (b->n < 0 || (b->n > 0 && !b->ts)) return fail(a, CEP_E_ARG, "bad batch");
+  if (b->n == 0) return CEP_OK;
+  if (b->input < 0 || b->input >= (int)a->app.inputs.size())
+    return fail(a, CEP_E_UNDEFINED_STREAM, "undefined input handle");
+  const StreamSchema& sd = a->app.inputs[b->input];
+  if (b->ncols != (int)sd.attrs.size() || b->ncols > kMaxCols)
+    return fail(a, CEP_E_ARG, "batch has " + std::to_string(b->ncols) + " columns, stream " +
+                                  sd.id + " defines " + std::to_string(sd.attrs.size()));
+  RowsArgs rows{};
+  rows.cols.n = b->ncols;
+  for (int c = 0; c < b->ncols; ++c) rows.cols.t[c] = sd.attrs[c].type;
+  rows.input = b->input;
+  rows.row0 = 0;
+  rows.n = b->n;
+  rows.seq0 = a->events_in;
+  rows.prev_ts = a->last_ts;
+  if (b->on_device) {
+    for (int c = 0; c < b->ncols; ++c) rows.cols.p[c] = b->cols[c];
+    rows.ts = b->ts;
+    rows.stream = b->stream;
+  } else {
+    // host batch: stage into device memory (the PCIe-inclusive path)
+    size_t need = (size_t)b->ncols + 2;
+    if (a->stage.size() < need) a->stage.resize(need);
+    for (int c = 0; c < b->ncols; ++c) {
+      size_t bytes = (size_t)b->n * type_width(sd.attrs[c].type);
+      if (!dev_ensure(&a->stage[c], bytes, a->stream, false))
+        return fail(a, CEP_E_DEVICE, "out of device memory (staging)");
+      hipMemcpyAsync(a->stage[c].p, b->cols[c], bytes, hipMemcpyHostToDevice, a->stream);
+      rows.cols.p[c] = a->stage[c].p;
+    }
+    DevBuf& tsb = a->stage[b->ncols];
+    if (!dev_ensure(&tsb, (size_t)b->n * 8, a->stream, false))
+      return fail(a, CEP_E_DEVICE, "out of device memory (staging)");
+    hipMemcpyAsync(tsb.p, b->ts, (size_t)b->n * 8, hipMemcpyHostToDevice, a->stream);
+    rows.ts = (const int64_t*)tsb.p;
+    if (b->stream) {
+      DevBuf& sb = a->stage[b->ncols + 1];
+      if (!dev_ensure(&sb, (size_t)b->n, a->stream, false))
+        return fail(a, CEP_E_DEVICE, "out of device memory (staging)");
+      hipMemcpyAsync(sb.p, b->stream, (size_t)b->n, hipMemcpyHostToDevice, a->stream);
+      rows.stream = (const uint8_t*)sb.p;
+    }
+    a->last_ts = b->ts[b->n - 1];
+  }
+  if (b->on_device) {
+    // last ts for cross-batch order checks: read the final element asynchronously
+    // is not worth a sync; the in-batch check covers the hot path.
+    a->last_ts = INT64_MIN;
+  }
+  a->events_in += b->n;
+  a->batches++;
+  int rc = send_device_rows(a, rows);
+  if (b->on_device == 0) hipStreamSynchronize(a->stream);   // host buffers may be reused
+  return rc;
+}
+
+int cep_flush(cep_app* a) {
+  if (!a) return CEP_E_ARG;
+  if (hipStreamSynchronize(a->stream) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "device failure during processing");
+  harvest_timers(a);
+  int rc = check_device_error(a);
+  for (auto& o : a->outs) {
+    unsigned long long cnt = 0;
+    hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
+    if (cnt > (unsigned long long)o.cap) cnt = o.cap;
+    a->matches_out += (int64_t)cnt;
+    if (o.fn && cnt > 0 && rc == CEP_OK) {
+      const size_t n = cnt;
+      o.hcols.resize(o.cols.size());
+      std::vector<const void*> ptrs(o.cols.size());
+      o.hts.resize(n);
+      o.hseq.resize(n);
+      hipMemcpy(o.hts.data(), o.ts.p, n * 8, hipMemcpyDeviceToHost);
+      hipMemcpy(o.hseq.data(), o.seq.p, n * 8, hipMemcpyDeviceToHost);
+      for (size_t c = 0; c < o.cols.size(); ++c) {
+        o.hcols[c].resize(n * type_width(o.types[c]));
+        hipMemcpy(o.hcols[c].data(), o.cols[c].p, o.hcols[c].size(), hipMemcpyDeviceToHost);
+      }
+      if (a->opt.ordered_output) {
+        // Siddhi's emission order: by completing event, then by pending
+        // order (contiguous per key already) — a stable sort on seq.
+        std::vector<uint32_t> perm(n);
+        std::iota(perm.begin(), perm.end(), 0u);
+        bool sorted = std::is_sorted(o.hseq.begin(), o.hseq.end());
+        if (!sorted) {
+          std::stable_sort(perm.begin(), perm.end(),
+                           [&](uint32_t x, uint32_t y) { return o.hseq[x] < o.hseq[y]; });
+          auto apply = [&](std::vector<uint8_t>& col, int w) {
+            std::vector<uint8_t> tmp(col.size());
+            for (size_t i = 0; i < n; ++i) std::memcpy(&tmp[i * w], &col[(size_t)perm[i] * w], w);
+            col.swap(tmp);
+          };
+          for (size_t c = 0; c < o.cols.size(); ++c) apply(o.hcols[c], type_width(o.types[c]));
+          std::vector<int64_t> t2(n), s2(n);
+          for (size_t i = 0; i < n; ++i) {
+            t2[i] = o.hts[perm[i]];
+            s2[i] = o.hseq[perm[i]];
+          }
+          o.hts.swap(t2);
+          o.hseq.swap(s2);
+        }
+      }
+      for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.hcols[c].data();
+      cep_rows rows{};
+      rows.stream_id = o.id.c_str();
+      rows.n = (int64_t)n;
+      rows.ncols = (int32_t)o.cols.size();
+      rows.ts = o.hts.data();
+      rows.seq = o.hseq.data();
+      rows.cols = ptrs.data();
+      o.fn(o.user, &rows);
+    }
+    hipMemset(o.count, 0, sizeof(unsigned long long));
+    o.bound = 0;
+  }
+  return rc;
+}
+
+int cep_output_device(cep_app* a, const char* out_id, cep_rows* rows) {
+  if (!a || !out_id || !rows) return CEP_E_ARG;
+  int i = a->app.output_index(out_id);
+  if (i < 0) return fail(a, CEP_E_UNDEFINED_STREAM, std::string("Stream ") + out_id + " not defined");
+  if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "device failure");
+  harvest_timers(a);
+  int rc = check_device_error(a);
+  if (rc) return rc;
+  OutStream& o = a->outs[i];
+  unsigned long long cnt = 0;
+  hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
+  static thread_local std::vector<const void*> ptrs;
+  ptrs.assign(o.cols.size(), nullptr);
+  for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.cols[c].p;
+  rows->stream_id = o.id.c_str();
+  rows->n = (int64_t)std::min<unsigned long long>(cnt, (unsigned long long)o.cap);
+  rows->ncols = (int32_t)o.cols.size();
+  rows->ts = (const int64_t*)o.ts.p;
+  rows->seq = (const int64_t*)o.seq.p;
+  rows->cols = ptrs.data();
+  return CEP_OK;
+}
+
+int cep_reset_output(cep_app* a) {
+  if (!a) return CEP_E_ARG;
+  for (auto& o : a->outs) {
+    hipMemsetAsync(o.count, 0, sizeof(unsigned long long), a->stream);
+    o.bound = 0;
+  }
+  return CEP_OK;
+}
+
+int cep_set_enabled(cep_app* a, int enabled) {
+  if (!a) return CEP_E_ARG;
+  a->enabled = enabled != 0;
+  return CEP_OK;
+}
+
+int32_t cep_dict_intern(cep_app* a, const char* s) {
+  if (!a || !s) return -1;
+  auto it = a->dict_index.find(s);
+  if (it != a->dict_index.end()) return it->second;
+  int32_t id = (int32_t)a->dict.size();
+  a->dict.push_back(s);
+  a->dict_index.emplace(s, id);
+  return id;
+}
+
+const char* cep_dict_lookup(cep_app* a, int32_t id) {
+  if (!a || id < 0 || id >= (int32_t)a->dict.size()) return nullptr;
+  return a->dict[id].c_str();
+}
+
+int cep_stats(cep_app* a, cep_stats_t* s) {
+  if (!a || !s) return CEP_E_ARG;
+  hipStreamSynchronize(a->stream);
+  harvest_timers(a);
+  std::memset(s, 0, sizeof(*s));
+  s->events_in = a->events_in;
+  s->matches_out = a->matches_out;
+  s->batches = a->batches;
+  for (int i = 0; i < 8; ++i) {
+    s->kernel_launches[i] = a->launches[i];
+    s->kernel_ms[i] = a->kernel_ms[i];
+  }
+  return CEP_OK;
+}
+
+const char* cep_last_error(cep_app* a) { return a ? a->last_error.c_str() : "null app"; }
+
+void cep_free(void* p) { std::free(p); }
+
+// Snapshot format (little endian):
+//   "CEPS" u32 version=1, u64 plan_hash, i64 events_in, u32 n_patterns,
+//   per pattern: i64 key_capacity, u32 S, u32 slot_words, u32 n_live,
+//                n_live x { u32 key, u8 cnt, u8 started, cnt*slot_words u64 }
+static uint64_t plan_hash(const CompiledApp& app) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  };
+  mix(app.code.data(), app.code.size() * sizeof(Ins));
+  mix(app.konst.data(), app.konst.size() * 8);
+  return h;
+}
+
+int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
+  if (!a || !buf || !len) return CEP_E_ARG;
+  if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "device failure");
+  std::vector<uint8_t> out;
+  auto put = [&](const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    out.insert(out.end(), b, b + n);
+  };
+  const char magic[4] = {'C', 'E', 'P', 'S'};
+  put(magic, 4);
+  uint32_t ver = 1;
+  put(&ver, 4);
+  uint64_t h = plan_hash(a->app);
+  put(&h, 8);
+  put(&a->events_in, 8);
+  uint32_t np = (uint32_t)a->pats.size();
+  put(&np, 4);
+  for (auto& rt : a->pats) {
+    const int64_t kc = rt.pa.key_capacity;
+    const uint32_t S = rt.pa.pending_slots, sw = rt.pa.slot_words;
+    std::vector<uint8_t> cnt(kc), st(kc);
+    hipMemcpy(cnt.data(), rt.pcnt.p, kc, hipMemcpyDeviceToHost);
+    hipMemcpy(st.data(), rt.started.p, kc, hipMemcpyDeviceToHost);
+    std::vector<uint64_t> slots((size_t)kc * S * sw);
+    hipMemcpy(slots.data(), rt.slots.p, slots.size() * 8, hipMemcpyDeviceToHost);
+    uint32_t live = 0;
+    for (int64_t k = 0; k < kc; ++k) live += (cnt[k] || st[k]) ? 1 : 0;
+    put(&kc, 8);
+    put(&S, 4);
+    put(&sw, 4);
+    put(&live, 4);
+    for (int64_t k = 0; k < kc; ++k) {
+      if (!cnt[k] && !st[k]) continue;
+      uint32_t key = (uint32_t)k;
+      put(&key, 4);
+      put(&cnt[k], 1);
+      put(&st[k], 1);
+      put(&slots[(size_t)k * S * sw], (size_t)cnt[k] * sw * 8);
+    }
+  }
+  *buf = (uint8_t*)std::malloc(out.size());
+  if (!*buf) return fail(a, CEP_E_DEVICE, "out of host memory");
+  std::memcpy(*buf, out.data(), out.size());
+  *len = out.size();
+  return CEP_OK;
+}
+
+int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
+  if (!a || (!buf && len)) return CEP_E_ARG;
+  size_t off = 0;
+  auto get = [&](void* p, size_t n) -> bool {
+    if (off + n > len) return false;
+    std::memcpy(p, buf + off, n);
+    off += n;
+    return true;
+  };
+  char magic[4];
+  uint32_t ver;
+  uint64_t h;
+  int64_t ev;
+  uint32_t np;
+  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver != 1 || !get(&h, 8) ||
+      !get(&ev, 8) || !get(&np, 4))
+    return fail(a, CEP_E_STATE, "not a libcep snapshot");
+  if (h != plan_hash(a->app) || np != a->pats.size())
+    return fail(a, CEP_E_STATE, "snapshot was taken with a different plan");
+  hipStreamSynchronize(a->stream);
+  for (auto& rt : a->pats) {
+    int64_t kc;
+    uint32_t S, sw, live;
+    if (!get(&kc, 8) || !get(&S, 4) || !get(&sw, 4) || !get(&live, 4))
+      return fail(a, CEP_E_STATE, "truncated snapshot");
+    if (kc != rt.pa.key_capacity || S != (uint32_t)rt.pa.pending_slots ||
+        sw != (uint32_t)rt.pa.slot_words)
+      return fail(a, CEP_E_STATE, "snapshot geometry differs from this runtime");
+    std::vector<uint8_t> cnt(kc, 0), st(kc, 0);
+    std::vector<uint64_t> slots((size_t)kc * S * sw, 0);
+    for (uint32_t i = 0; i < live; ++i) {
+      uint32_t key;
+      uint8_t c, s;
+      if (!get(&key, 4) || !get(&c, 1) || !get(&s, 1) || key >= kc || c > S)
+        return fail(a, CEP_E_STATE, "corrupt snapshot");
+      cnt[key] = c;
+      st[key] = s;
+      if (!get(&slots[(size_t)key * S * sw], (size_t)c * sw * 8))
+        return fail(a, CEP_E_STATE, "truncated snapshot");
+    }
+    hipMemcpy(rt.pcnt.p, cnt.data(), kc, hipMemcpyHostToDevice);
+    hipMemcpy(rt.started.p, st.data(), kc, hipMemcpyHostToDevice);
+    hipMemcpy(rt.slots.p, slots.data(), slots.size() * 8, hipMemcpyHostToDevice);
+  }
+  a->events_in = ev;
+  return CEP_OK;
+}
+
+int cep_record_words(cep_app* a) {
+  if (!a || a->pats.size() != 1) return -CEP_E_UNSUPPORTED;
+  return a->pats[0].pa.rec_words;
+}
+
+int cep_route_batch(cep_app* a, const cep_batch* b, int world, void* rec_out, int64_t rec_cap,
+                    int64_t* counts_host) {
+  (void)a; (void)b; (void)world; (void)rec_out; (void)rec_cap; (void)counts_host;
+  return CEP_E_UNSUPPORTED;
+}
+
+int cep_send_records(cep_app* a, const void* recs, int64_t n, int64_t events_represented) {
+  (void)a; (void)recs; (void)n; (void)events_represented;
+  return CEP_E_UNSUPPORTED;
+}
+
+int cep_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys, int64_t rate, int64_t t0,
+                 int single_stream, int32_t* key, int64_t* ts, uint8_t* stream, int32_t* id,
+                 double* price, void* hip_stream) {
+  if (n < 0 || keys <= 0 || rate <= 0) return CEP_E_ARG;
+  launch_generate(first, n, seed, keys, rate, t0, single_stream, key, ts, stream, id, price,
+                  (hipStream_t)hip_stream);
+  return hipGetLastError() == hipSuccess ? CEP_OK : CEP_E_DEVICE;
+}
+
+}  // extern "C"

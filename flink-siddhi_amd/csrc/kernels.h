@@ -1,0 +1,140 @@
+// Kernel argument blocks and launchers for the gfx950 kernels in kernels.hip.
+// Host code (engine.cpp) fills these from a CompiledApp; everything is passed
+// by value as kernel arguments (no per-launch allocation: graph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "plan.h"
+
+namespace cep {
+
+// Columns of one input batch, in stream-definition order.
+struct ColSet {
+  const void* p[kMaxCols];
+  int32_t t[kMaxCols];
+  int32_t n;
+};
+
+// A contiguous slice [row0, row0 + n) of an input batch.
+struct RowsArgs {
+  ColSet cols;
+  const int64_t* ts;
+  const uint8_t* stream;   // per-row input handle, or nullptr
+  int32_t input;           // handle when stream == nullptr
+  int64_t row0;            // first row of the slice within the batch
+  int64_t n;               // rows in the slice
+  int64_t seq0;            // arrival sequence number of batch row 0
+  int64_t prev_ts;         // ts of the row before the slice (monotonicity check)
+};
+
+struct VmArgs {
+  const Ins* code;
+  const uint64_t* konst;
+};
+
+// Output columns of one output stream (device).
+struct OutArgs {
+  void* col[kMaxOut];
+  int32_t type[kMaxOut];
+  int32_t prog[kMaxOut];   // program offset per output attribute
+  int32_t ncols;
+  int64_t* ts;
+  int64_t* seq;
+  unsigned long long* count;   // rows written so far (atomic cursor)
+  int64_t cap;
+};
+
+// Error flags (device word, OR-ed).
+enum : uint32_t {
+  ERR_KEY_RANGE = 1u,        // partition / group key outside [0, key_capacity)
+  ERR_PENDING = 2u,          // per-key pending capacity exceeded
+  ERR_ORDER = 4u,            // ts decreased inside a batch (within needs event-time order)
+  ERR_OUT_CAP = 8u,          // output capacity exceeded (engine sizing bug)
+  ERR_WINDOW = 16u,          // bucket window logic error
+};
+
+// ---------------------------------------------------------------- filter --
+struct FilterArgs {
+  RowsArgs rows;
+  VmArgs vm;
+  int32_t in_stream;
+  int32_t filter_prog;     // -1: no filter
+  OutArgs out;
+  unsigned long long* tile_state;   // decoupled look-back words (zeroed per launch)
+  unsigned int* ticket;             // tile ticket counter (zeroed per launch)
+  unsigned int* err;
+};
+
+// ------------------------------------------------------- keyed pattern --
+// `[every] s1=A[f] -> s2=B[g] [within W]` under `partition with`.
+struct PatternArgs {
+  int32_t a_stream, b_stream;
+  int32_t f_prog;          // -1: true
+  int32_t g_raw_prog;      // g evaluated in the partition pass (-1: true / in walk)
+  int32_t g_walk_prog;     // g evaluated per (pending, B) in the walk (-1: none)
+  int32_t every;
+  int64_t within;          // -1: none
+  int32_t key_col_a, key_col_b;   // -1: unpartitioned (single key 0)
+  int32_t nrec_a, nrec_b;
+  int32_t rec_a[kMaxCaps], rec_b[kMaxCaps];   // columns carried in records
+  int32_t ncap;                                // captured words per pending slot
+  int32_t cap_from_rec[kMaxCaps];
+  int32_t rec_words;       // 3 + max(nrec_a, nrec_b)
+  int32_t slot_words;      // 2 + ncap
+  int32_t pending_slots;   // S
+  int64_t key_capacity;    // dense keys per shard
+  int32_t key_stride, key_offset;   // shard ownership (key % stride == offset)
+  int32_t buckets_log2;
+};
+
+struct PartArgs {
+  RowsArgs rows;
+  VmArgs vm;
+  PatternArgs pat;
+  int32_t from_records;        // 1: input rows are records (multi-GPU receive)
+  const uint64_t* in_recs;     // records when from_records
+  int32_t tile_rows;           // rows per tile (2048)
+  uint64_t* recs;              // out: records, tile-major
+  uint16_t* tile_off;          // out: [ntiles][P+1] exclusive offsets
+  int32_t route_world;         // >0: route mode — bucket = owner shard, no key_local
+  unsigned int* err;
+};
+
+struct WalkArgs {
+  VmArgs vm;
+  PatternArgs pat;
+  const uint64_t* recs;
+  const uint16_t* tile_off;
+  int32_t ntiles;
+  int32_t tile_rows;
+  int64_t seq_chunk0;          // sequence number of the chunk's first row
+  // per-key state (global, dense key index)
+  uint8_t* pcnt;
+  uint8_t* started;
+  uint64_t* slots;             // [key][S][slot_words]
+  OutArgs out;
+  unsigned int* err;
+};
+
+// --------------------------------------------------------------- launchers --
+void launch_filter(const FilterArgs& a, int64_t ntiles, hipStream_t s);
+void launch_partition(const PartArgs& a, int64_t ntiles, hipStream_t s);
+void launch_walk(const WalkArgs& a, int nbuckets, hipStream_t s);
+void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
+                     int64_t rate, int64_t t0, int single_stream, int32_t* key,
+                     int64_t* ts, uint8_t* stream, int32_t* id, double* price,
+                     hipStream_t s);
+
+constexpr int kFilterThreads = 256;
+constexpr int kFilterItems = 16;          // rows per thread per tile
+constexpr int kPartThreads = 256;
+constexpr int kPartItems = 8;             // tile = 2048 rows
+constexpr int kWalkThreads = 256;
+constexpr int kWalkWindow = 2048;         // records per LDS window
+constexpr int kWalkMaxTiles = 2048;       // tiles per chunk
+constexpr int kWalkMaxKeys = 1024;        // keys per bucket (LDS histogram)
+constexpr int kMaxPending = 32;           // pending_slots upper bound
+
+}  // namespace cep

@@ -1,0 +1,299 @@
+// Device-side interpreter for the predicate / projection programs of plan.h.
+//
+// Value semantics follow Siddhi's expression executors on Java primitives
+// (SURVEY.md App. A.2): int/long arithmetic wraps, int division truncates,
+// `%` takes the dividend's sign, int/long division or remainder by zero
+// yields null, a comparison with a null operand is false, float ops are
+// IEEE binary32, double ops IEEE binary64, NaN compares false.
+//
+// The register file lives in LDS laid out [reg][thread] (64 consecutive lanes
+// touch 64 consecutive 8-byte words: conflict-free ds_read_b64 / ds_write_b64),
+// so programs with runtime register operands never spill to scratch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "plan.h"
+
+namespace cep {
+
+__device__ __forceinline__ float as_f32(uint64_t v) { return __uint_as_float((uint32_t)v); }
+__device__ __forceinline__ double as_f64(uint64_t v) { return __longlong_as_double((long long)v); }
+__device__ __forceinline__ uint64_t from_f32(float f) { return (uint64_t)__float_as_uint(f); }
+__device__ __forceinline__ uint64_t from_f64(double d) { return (uint64_t)__double_as_longlong(d); }
+__device__ __forceinline__ uint64_t from_i32(int32_t i) { return (uint64_t)(int64_t)i; }
+
+// Load one element of a typed column as a VM word.
+__device__ __forceinline__ uint64_t load_col(const void* p, int type, int64_t row) {
+  switch (type) {
+    case T_LONG:
+    case T_DOUBLE:
+      return ((const uint64_t*)p)[row];
+    case T_BOOL:
+      return ((const uint8_t*)p)[row] ? 1u : 0u;
+    case T_FLOAT:
+      return (uint64_t)((const uint32_t*)p)[row];
+    default:  // INT, STRING (dictionary id)
+      return from_i32(((const int32_t*)p)[row]);
+  }
+}
+
+__device__ __forceinline__ void store_col(void* p, int type, int64_t row, uint64_t v) {
+  switch (type) {
+    case T_LONG:
+    case T_DOUBLE:
+      ((uint64_t*)p)[row] = v;
+      break;
+    case T_BOOL:
+      ((uint8_t*)p)[row] = (uint8_t)(v & 1);
+      break;
+    default:
+      ((uint32_t*)p)[row] = (uint32_t)v;
+      break;
+  }
+}
+
+__device__ __forceinline__ uint64_t vm_convert(uint64_t v, int from, int to) {
+  if (from == to) return v;
+  if (to == T_LONG) return v;  // int words are already sign-extended
+  if (to == T_FLOAT) {
+    if (from == T_INT) return from_f32((float)(int32_t)v);
+    if (from == T_LONG) return from_f32((float)(int64_t)v);
+    return v;
+  }
+  if (to == T_DOUBLE) {
+    if (from == T_INT) return from_f64((double)(int32_t)v);
+    if (from == T_LONG) return from_f64((double)(int64_t)v);
+    if (from == T_FLOAT) return from_f64((double)as_f32(v));
+  }
+  return v;
+}
+
+// Arithmetic; returns false when the result is null (int div/mod by zero).
+__device__ __forceinline__ bool vm_arith(int op, int t, uint64_t a, uint64_t b, uint64_t* r) {
+  switch (t) {
+    case T_INT: {
+      int32_t x = (int32_t)a, y = (int32_t)b;
+      uint32_t ux = (uint32_t)x, uy = (uint32_t)y;
+      int32_t z;
+      switch (op) {
+        case OP_ADD: z = (int32_t)(ux + uy); break;
+        case OP_SUB: z = (int32_t)(ux - uy); break;
+        case OP_MUL: z = (int32_t)(ux * uy); break;
+        case OP_DIV:
+          if (y == 0) return false;
+          z = (y == -1) ? (int32_t)(0u - ux) : x / y;
+          break;
+        default:
+          if (y == 0) return false;
+          z = (y == -1) ? 0 : x % y;
+          break;
+      }
+      *r = from_i32(z);
+      return true;
+    }
+    case T_LONG: {
+      int64_t x = (int64_t)a, y = (int64_t)b;
+      uint64_t z;
+      switch (op) {
+        case OP_ADD: z = a + b; break;
+        case OP_SUB: z = a - b; break;
+        case OP_MUL: z = a * b; break;
+        case OP_DIV:
+          if (y == 0) return false;
+          z = (y == -1) ? (0ull - a) : (uint64_t)(x / y);
+          break;
+        default:
+          if (y == 0) return false;
+          z = (y == -1) ? 0ull : (uint64_t)(x % y);
+          break;
+      }
+      *r = z;
+      return true;
+    }
+    case T_FLOAT: {
+      float x = as_f32(a), y = as_f32(b), z;
+      switch (op) {
+        case OP_ADD: z = x + y; break;
+        case OP_SUB: z = x - y; break;
+        case OP_MUL: z = x * y; break;
+        case OP_DIV: z = x / y; break;
+        default: z = fmodf(x, y); break;
+      }
+      *r = from_f32(z);
+      return true;
+    }
+    default: {
+      double x = as_f64(a), y = as_f64(b), z;
+      switch (op) {
+        case OP_ADD: z = x + y; break;
+        case OP_SUB: z = x - y; break;
+        case OP_MUL: z = x * y; break;
+        case OP_DIV: z = x / y; break;
+        default: z = fmod(x, y); break;
+      }
+      *r = from_f64(z);
+      return true;
+    }
+  }
+}
+
+__device__ __forceinline__ bool vm_compare(int op, int t, uint64_t a, uint64_t b) {
+  switch (t) {
+    case T_LONG: {
+      int64_t x = (int64_t)a, y = (int64_t)b;
+      switch (op) {
+        case OP_EQ: return x == y;
+        case OP_NE: return x != y;
+        case OP_LT: return x < y;
+        case OP_LE: return x <= y;
+        case OP_GT: return x > y;
+        default: return x >= y;
+      }
+    }
+    case T_FLOAT: {
+      float x = as_f32(a), y = as_f32(b);
+      switch (op) {
+        case OP_EQ: return x == y;
+        case OP_NE: return x != y;
+        case OP_LT: return x < y;
+        case OP_LE: return x <= y;
+        case OP_GT: return x > y;
+        default: return x >= y;
+      }
+    }
+    case T_DOUBLE: {
+      double x = as_f64(a), y = as_f64(b);
+      switch (op) {
+        case OP_EQ: return x == y;
+        case OP_NE: return x != y;
+        case OP_LT: return x < y;
+        case OP_LE: return x <= y;
+        case OP_GT: return x > y;
+        default: return x >= y;
+      }
+    }
+    default: {  // INT, BOOL, STRING ids
+      int32_t x = (int32_t)a, y = (int32_t)b;
+      switch (op) {
+        case OP_EQ: return x == y;
+        case OP_NE: return x != y;
+        case OP_LT: return x < y;
+        case OP_LE: return x <= y;
+        case OP_GT: return x > y;
+        default: return x >= y;
+      }
+    }
+  }
+}
+
+// Evaluate program at `off`.  `R` is this block's LDS register file, `lane`
+// the thread's column in it, `stride` the block size.  Env supplies
+// col(c, type), cap(i), outv(i), agg(i), ts().  Returns the result word of
+// register 0; *is_null reports a null result.
+template <class Env>
+__device__ __forceinline__ uint64_t vm_eval(const Ins* __restrict__ code,
+                                            const uint64_t* __restrict__ konst, int off,
+                                            uint64_t* R, int lane, int stride,
+                                            const Env& env, bool* is_null) {
+  uint32_t nullm = 0;
+#define VREG(r) R[(r) * stride + lane]
+  for (int pc = off;; ++pc) {
+    const Ins in = code[pc];
+    const int d = in.dst, a = in.a, b = in.b;
+    switch (in.op) {
+      case OP_END:
+        *is_null = (nullm & 1u) != 0;
+        return VREG(0);
+      case OP_LDCOL:
+        VREG(d) = env.col((int)in.imm, b);
+        nullm &= ~(1u << d);
+        break;
+      case OP_LDTS:
+        VREG(d) = (uint64_t)env.ts();
+        nullm &= ~(1u << d);
+        break;
+      case OP_LDK:
+        VREG(d) = konst[in.imm];
+        nullm &= ~(1u << d);
+        break;
+      case OP_LDCAP:
+        VREG(d) = env.cap((int)in.imm);
+        nullm &= ~(1u << d);
+        break;
+      case OP_LDOUT: {
+        bool n = false;
+        VREG(d) = env.outv((int)in.imm, &n);
+        nullm = n ? (nullm | (1u << d)) : (nullm & ~(1u << d));
+        break;
+      }
+      case OP_LDAGG: {
+        bool n = false;
+        VREG(d) = env.agg((int)in.imm, &n);
+        nullm = n ? (nullm | (1u << d)) : (nullm & ~(1u << d));
+        break;
+      }
+      case OP_CVT:
+        VREG(d) = vm_convert(VREG(a), (int)(in.imm >> 8), (int)(in.imm & 0xff));
+        nullm = (nullm & (1u << a)) ? (nullm | (1u << d)) : (nullm & ~(1u << d));
+        break;
+      case OP_ADD:
+      case OP_SUB:
+      case OP_MUL:
+      case OP_DIV:
+      case OP_MOD: {
+        uint64_t r = 0;
+        bool nn = ((nullm >> a) | (nullm >> b)) & 1u;
+        if (!nn) nn = !vm_arith(in.op, (int)in.imm, VREG(a), VREG(b), &r);
+        VREG(d) = r;
+        nullm = nn ? (nullm | (1u << d)) : (nullm & ~(1u << d));
+        break;
+      }
+      case OP_NEG: {
+        uint64_t v = VREG(a), r;
+        switch ((int)in.imm) {
+          case T_INT: r = from_i32((int32_t)(0u - (uint32_t)v)); break;
+          case T_LONG: r = 0ull - v; break;
+          case T_FLOAT: r = from_f32(-as_f32(v)); break;
+          default: r = from_f64(-as_f64(v)); break;
+        }
+        VREG(d) = r;
+        nullm = (nullm & (1u << a)) ? (nullm | (1u << d)) : (nullm & ~(1u << d));
+        break;
+      }
+      case OP_EQ:
+      case OP_NE:
+      case OP_LT:
+      case OP_LE:
+      case OP_GT:
+      case OP_GE: {
+        bool nn = ((nullm >> a) | (nullm >> b)) & 1u;
+        VREG(d) = (!nn && vm_compare(in.op, (int)in.imm, VREG(a), VREG(b))) ? 1u : 0u;
+        nullm &= ~(1u << d);
+        break;
+      }
+      case OP_AND:
+        VREG(d) = ((VREG(a) & 1u) && !((nullm >> a) & 1u) && (VREG(b) & 1u) &&
+                   !((nullm >> b) & 1u)) ? 1u : 0u;
+        nullm &= ~(1u << d);
+        break;
+      case OP_OR:
+        VREG(d) = (((VREG(a) & 1u) && !((nullm >> a) & 1u)) ||
+                   ((VREG(b) & 1u) && !((nullm >> b) & 1u))) ? 1u : 0u;
+        nullm &= ~(1u << d);
+        break;
+      case OP_NOT:
+        VREG(d) = ((VREG(a) & 1u) && !((nullm >> a) & 1u)) ? 0u : 1u;
+        nullm &= ~(1u << d);
+        break;
+      default:  // OP_MOV
+        VREG(d) = VREG(a);
+        nullm = (nullm & (1u << a)) ? (nullm | (1u << d)) : (nullm & ~(1u << d));
+        break;
+    }
+  }
+#undef VREG
+}
+
+}  // namespace cep

@@ -1,0 +1,183 @@
+"""ctypes binding of libcep.so (include/cep.h).
+
+This is the Python analogue of the JNI/Panama stub a Java maintainer would add
+(INTEGRATION.md).  It fails loudly when libcep.so is missing — there is no
+CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("CEP_LIB", str(_HERE.parent / "libcep.so")))
+
+CEP_OK = 0
+CEP_E_PARSE = 1
+CEP_E_UNDEFINED_STREAM = 2
+CEP_E_DUPLICATED_STREAM = 3
+CEP_E_UNSUPPORTED = 4
+CEP_E_ARG = 5
+CEP_E_DEVICE = 6
+CEP_E_CAPACITY = 7
+CEP_E_STATE = 8
+
+INT, LONG, FLOAT, DOUBLE, BOOL, STRING, OBJECT = range(7)
+TYPE_NAMES = {INT: "int", LONG: "long", FLOAT: "float", DOUBLE: "double",
+              BOOL: "bool", STRING: "string", OBJECT: "object"}
+NUMPY_DTYPES = {INT: "int32", LONG: "int64", FLOAT: "float32",
+                DOUBLE: "float64", BOOL: "uint8", STRING: "int32"}
+
+K_FILTER, K_PARTITION, K_WALK, K_ROUTE, K_ORDER, K_AGG, K_OTHER = range(7)
+
+
+# ---- exceptions mirroring the reference ---------------------------------
+class SiddhiError(RuntimeError):
+    code = -1
+
+
+class SiddhiAppCreationException(SiddhiError):
+    """Parse / validation failure (SiddhiManager.validateSiddhiApp,
+    AbstractSiddhiOperator.java:292-299)."""
+    code = CEP_E_PARSE
+
+
+class UndefinedStreamException(SiddhiError):
+    """exception/UndefinedStreamException.java:20."""
+    code = CEP_E_UNDEFINED_STREAM
+
+
+class DuplicatedStreamException(SiddhiError):
+    """exception/DuplicatedStreamException.java:20."""
+    code = CEP_E_DUPLICATED_STREAM
+
+
+class UnsupportedPlanException(SiddhiError):
+    """Valid SiddhiQL outside the device subset (joins, windows, tables)."""
+    code = CEP_E_UNSUPPORTED
+
+
+class CepDeviceError(SiddhiError):
+    code = CEP_E_DEVICE
+
+
+class CepCapacityError(SiddhiError):
+    code = CEP_E_CAPACITY
+
+
+class CepStateError(SiddhiError):
+    code = CEP_E_STATE
+
+
+_EXC = {CEP_E_PARSE: SiddhiAppCreationException,
+        CEP_E_UNDEFINED_STREAM: UndefinedStreamException,
+        CEP_E_DUPLICATED_STREAM: DuplicatedStreamException,
+        CEP_E_UNSUPPORTED: UnsupportedPlanException,
+        CEP_E_ARG: ValueError, CEP_E_DEVICE: CepDeviceError,
+        CEP_E_CAPACITY: CepCapacityError, CEP_E_STATE: CepStateError}
+
+
+def raise_for(code: int, msg: str):
+    if code == CEP_OK:
+        return
+    exc = _EXC.get(code, SiddhiError)
+    raise exc(msg)
+
+
+# ---- structs ---------------------------------------------------------------
+class cep_attr(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("type", C.c_int32)]
+
+
+class cep_options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("pending_slots", C.c_int32),
+                ("key_capacity", C.c_int64), ("chunk_events", C.c_int64),
+                ("buckets_log2", C.c_int32), ("profile", C.c_int32),
+                ("ordered_output", C.c_int32), ("key_stride", C.c_int32),
+                ("key_offset", C.c_int32), ("reserved", C.c_int32 * 7)]
+
+
+class cep_batch(C.Structure):
+    _fields_ = [("n", C.c_int64), ("ts", C.c_void_p), ("stream", C.c_void_p),
+                ("input", C.c_int32), ("ncols", C.c_int32),
+                ("cols", C.POINTER(C.c_void_p)), ("on_device", C.c_int32)]
+
+
+class cep_rows(C.Structure):
+    _fields_ = [("stream_id", C.c_char_p), ("n", C.c_int64),
+                ("ncols", C.c_int32), ("ts", C.POINTER(C.c_int64)),
+                ("seq", C.POINTER(C.c_int64)),
+                ("cols", C.POINTER(C.c_void_p))]
+
+
+class cep_stats_t(C.Structure):
+    _fields_ = [("events_in", C.c_int64), ("matches_out", C.c_int64),
+                ("batches", C.c_int64), ("kernel_launches", C.c_int64 * 8),
+                ("kernel_ms", C.c_double * 8)]
+
+
+EMIT_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(cep_rows))
+
+# Every symbol include/cep.h declares, with its ctypes signature.
+SIGNATURES = {
+    "cep_default_options": (None, [C.POINTER(cep_options)]),
+    "cep_validate": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "cep_plan_schema": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(cep_attr),
+                                  C.c_int, C.POINTER(C.c_int), C.c_char_p,
+                                  C.c_size_t]),
+    "cep_create": (C.c_void_p, [C.c_char_p, C.POINTER(cep_options), C.c_char_p,
+                                C.c_size_t]),
+    "cep_destroy": (None, [C.c_void_p]),
+    "cep_stream_schema": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(cep_attr),
+                                    C.c_int, C.POINTER(C.c_int)]),
+    "cep_input": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "cep_set_callback": (C.c_int, [C.c_void_p, C.c_char_p, EMIT_FN, C.c_void_p]),
+    "cep_send_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch)]),
+    "cep_flush": (C.c_int, [C.c_void_p]),
+    "cep_output_device": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(cep_rows)]),
+    "cep_reset_output": (C.c_int, [C.c_void_p]),
+    "cep_snapshot": (C.c_int, [C.c_void_p, C.POINTER(C.POINTER(C.c_uint8)),
+                               C.POINTER(C.c_size_t)]),
+    "cep_restore": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "cep_free": (None, [C.c_void_p]),
+    "cep_set_enabled": (C.c_int, [C.c_void_p, C.c_int]),
+    "cep_dict_intern": (C.c_int32, [C.c_void_p, C.c_char_p]),
+    "cep_dict_lookup": (C.c_char_p, [C.c_void_p, C.c_int32]),
+    "cep_stats": (C.c_int, [C.c_void_p, C.POINTER(cep_stats_t)]),
+    "cep_last_error": (C.c_char_p, [C.c_void_p]),
+    "cep_record_words": (C.c_int, [C.c_void_p]),
+    "cep_route_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int,
+                                  C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "cep_send_records": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
+    "cep_generate": (C.c_int, [C.c_int64, C.c_int64, C.c_uint64, C.c_int64,
+                               C.c_int64, C.c_int64, C.c_int, C.c_void_p,
+                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                               C.c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(
+                "libcep.so not found at %s — build it with `make -C "
+                "flink-siddhi_amd` (or __graft_entry__.build())" % LIB_PATH)
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def default_options(**kw) -> cep_options:
+    o = cep_options()
+    lib().cep_default_options(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o

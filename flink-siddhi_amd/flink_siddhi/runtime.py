@@ -1,0 +1,238 @@
+"""Siddhi-runtime-shaped Python wrapper over libcep (C ABI).
+
+`SiddhiAppRuntime` mirrors the Siddhi calls flink-siddhi makes
+(SURVEY.md §8b): getInputHandler / InputHandler.send, addCallback, snapshot,
+shutdown — but batched and columnar: rows go in as numpy arrays (host) or
+torch CUDA tensors (device-resident), matches come out through callbacks at
+flush(), in Siddhi's emission order.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+def validate(plan: str) -> None:
+    """SiddhiManager.validateSiddhiApp (AbstractSiddhiOperator.java:292-299)."""
+    err = C.create_string_buffer(1024)
+    rc = L.lib().cep_validate(plan.encode(), err, len(err))
+    L.raise_for(rc, err.value.decode())
+
+
+def plan_schema(plan: str, stream_id: str):
+    """SiddhiTypeFactory.getStreamDefinition (utils/SiddhiTypeFactory.java:64-84):
+    [(name, type_name)] of any input or output stream of `plan`."""
+    err = C.create_string_buffer(1024)
+    attrs = (L.cep_attr * 64)()
+    n = C.c_int(0)
+    rc = L.lib().cep_plan_schema(plan.encode(), stream_id.encode(), attrs, 64,
+                                 C.byref(n), err, len(err))
+    L.raise_for(rc, err.value.decode())
+    return [(attrs[i].name.decode(), L.TYPE_NAMES[attrs[i].type])
+            for i in range(n.value)]
+
+
+@dataclass
+class OutputRows:
+    stream_id: str
+    ts: np.ndarray
+    seq: np.ndarray
+    cols: List[np.ndarray]
+
+    def __len__(self):
+        return len(self.ts)
+
+    def rows(self):
+        return [tuple(c[i].item() for c in self.cols) for i in range(len(self.ts))]
+
+
+class SiddhiAppRuntime:
+    """createSiddhiAppRuntime(plan) + start() (AbstractSiddhiOperator.java:120-142)."""
+
+    def __init__(self, plan: str, **options):
+        self._lib = L.lib()
+        self.options = L.default_options(**options)
+        err = C.create_string_buffer(2048)
+        h = self._lib.cep_create(plan.encode(), C.byref(self.options), err, len(err))
+        if not h:
+            msg = err.value.decode()
+            # map the creation failure onto the reference's exception family
+            code = L.CEP_E_PARSE
+            vrc = self._lib.cep_validate(plan.encode(), None, 0)
+            if vrc != L.CEP_OK:
+                code = vrc
+            elif "device" in msg.lower() or "gfx950" in msg or "HIP" in msg:
+                code = L.CEP_E_DEVICE
+            elif "capacity" in msg.lower() or "pending_slots" in msg:
+                code = L.CEP_E_CAPACITY
+            elif "not yet" in msg or "not supported" in msg:
+                code = L.CEP_E_UNSUPPORTED
+            L.raise_for(code, msg)
+        self._h = C.c_void_p(h)
+        self._callbacks: Dict[str, object] = {}
+        self._collected: Dict[str, List[OutputRows]] = {}
+
+    # -- lifecycle -----------------------------------------------------------
+    def shutdown(self):
+        if self._h:
+            self._lib.cep_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.shutdown()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != L.CEP_OK:
+            L.raise_for(rc, self._lib.cep_last_error(self._h).decode())
+
+    # -- schema ----------------------------------------------------------------
+    def stream_definition(self, stream_id: str):
+        attrs = (L.cep_attr * 64)()
+        n = C.c_int(0)
+        self._check(self._lib.cep_stream_schema(self._h, stream_id.encode(),
+                                                attrs, 64, C.byref(n)))
+        return [(attrs[i].name.decode(), attrs[i].type) for i in range(n.value)]
+
+    def input_handle(self, stream_id: str) -> int:
+        h = self._lib.cep_input(self._h, stream_id.encode())
+        if h < 0:
+            self._check(-h)
+        return h
+
+    def intern(self, s: str) -> int:
+        return self._lib.cep_dict_intern(self._h, s.encode())
+
+    def lookup(self, i: int) -> Optional[str]:
+        r = self._lib.cep_dict_lookup(self._h, int(i))
+        return None if r is None else r.decode()
+
+    # -- callbacks -------------------------------------------------------------
+    def add_callback(self, out_id: str,
+                     fn: Optional[Callable[[OutputRows], None]] = None):
+        """addCallback(outId, StreamCallback) (AbstractSiddhiOperator.java:165-166).
+        Without `fn`, rows are collected and returned by `collect(out_id)`."""
+        types = [t for _, t in self.stream_definition(out_id)]
+        self._collected.setdefault(out_id, [])
+
+        def cb(user, rows_p):
+            r = rows_p.contents
+            n = r.n
+            ts = np.ctypeslib.as_array(r.ts, shape=(n,)).copy() if n else np.zeros(0, np.int64)
+            seq = np.ctypeslib.as_array(r.seq, shape=(n,)).copy() if n else np.zeros(0, np.int64)
+            cols = []
+            for c, t in enumerate(types):
+                dt = np.dtype(L.NUMPY_DTYPES[t])
+                if n:
+                    buf = (C.c_char * (n * dt.itemsize)).from_address(r.cols[c])
+                    cols.append(np.frombuffer(buf, dtype=dt).copy())
+                else:
+                    cols.append(np.zeros(0, dt))
+            out = OutputRows(out_id, ts, seq, cols)
+            if fn is not None:
+                fn(out)
+            else:
+                self._collected[out_id].append(out)
+
+        cfn = L.EMIT_FN(cb)
+        self._callbacks[out_id] = cfn
+        self._check(self._lib.cep_set_callback(self._h, out_id.encode(), cfn, None))
+
+    def collect(self, out_id: str) -> OutputRows:
+        parts = self._collected.get(out_id, [])
+        self._collected[out_id] = []
+        types = [t for _, t in self.stream_definition(out_id)]
+        if not parts:
+            return OutputRows(out_id, np.zeros(0, np.int64), np.zeros(0, np.int64),
+                              [np.zeros(0, L.NUMPY_DTYPES[t]) for t in types])
+        return OutputRows(out_id, np.concatenate([p.ts for p in parts]),
+                          np.concatenate([p.seq for p in parts]),
+                          [np.concatenate([p.cols[c] for p in parts])
+                           for c in range(len(types))])
+
+    # -- input -----------------------------------------------------------------
+    def send(self, stream_id: str, ts, cols: Sequence, streams=None):
+        """A batch of InputHandler.send(ts, row) (AbstractSiddhiOperator.java:130).
+
+        `cols` follow the stream definition's attribute order.  numpy arrays
+        are host batches (staged over PCIe); torch CUDA tensors are
+        device-resident.  `streams` (uint8 per row: input handles) mixes
+        several identically-defined streams in one batch.
+        """
+        h = self.input_handle(stream_id)
+        defs = self.stream_definition(stream_id)
+        on_device = _is_device(ts)
+        keep = []
+        ptrs = (C.c_void_p * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            want = np.dtype(L.NUMPY_DTYPES[defs[i][1]]) if i < len(defs) else None
+            p, k = _ptr(c, want, on_device)
+            ptrs[i] = p
+            keep.append(k)
+        tsp, k = _ptr(ts, np.dtype("int64"), on_device)
+        keep.append(k)
+        sp = None
+        if streams is not None:
+            sp, k = _ptr(streams, np.dtype("uint8"), on_device)
+            keep.append(k)
+        b = L.cep_batch(n=_len(ts), ts=tsp, stream=sp, input=h, ncols=len(cols),
+                        cols=ptrs, on_device=1 if on_device else 0)
+        self._check(self._lib.cep_send_batch(self._h, C.byref(b)))
+
+    def flush(self):
+        self._check(self._lib.cep_flush(self._h))
+
+    def output_device(self, out_id: str):
+        r = L.cep_rows()
+        self._check(self._lib.cep_output_device(self._h, out_id.encode(), C.byref(r)))
+        return r
+
+    def reset_output(self):
+        self._check(self._lib.cep_reset_output(self._h))
+
+    def set_enabled(self, enabled: bool):
+        self._check(self._lib.cep_set_enabled(self._h, 1 if enabled else 0))
+
+    # -- state -------------------------------------------------------------------
+    def snapshot(self) -> bytes:
+        buf = C.POINTER(C.c_uint8)()
+        n = C.c_size_t(0)
+        self._check(self._lib.cep_snapshot(self._h, C.byref(buf), C.byref(n)))
+        try:
+            return C.string_at(buf, n.value)
+        finally:
+            self._lib.cep_free(buf)
+
+    def restore(self, data: bytes):
+        b = C.create_string_buffer(data, len(data))
+        self._check(self._lib.cep_restore(self._h, b, len(data)))
+
+    def stats(self) -> L.cep_stats_t:
+        s = L.cep_stats_t()
+        self._check(self._lib.cep_stats(self._h, C.byref(s)))
+        return s
+
+
+def _is_device(x) -> bool:
+    return hasattr(x, "is_cuda") and bool(x.is_cuda)
+
+
+def _len(x) -> int:
+    return int(x.shape[0]) if hasattr(x, "shape") else len(x)
+
+
+def _ptr(x, want_dtype, on_device):
+    if on_device:
+        if not _is_device(x):
+            raise ValueError("mixing host and device columns in one batch")
+        return C.c_void_p(x.data_ptr()), x
+    a = np.ascontiguousarray(x, dtype=want_dtype) if want_dtype is not None \
+        else np.ascontiguousarray(x)
+    return C.c_void_p(a.ctypes.data), a

@@ -1,0 +1,74 @@
+"""Synthetic keyed event streams.
+
+Counter-based, so host (numpy), device (libcep `cep_generate`) and any rank
+of a multi-GPU job produce the identical stream for any index range:
+
+    r(i, j) = splitmix64(seed ^ (i * 0x9E3779B97F4A7C15) ^ j),  seed = 0x5EEDC0DE
+    key    = r(i,0) mod K
+    stream = r(i,1) >> 63          (0 = A, 1 = B)
+    id     = r(i,2) mod 50         (RandomEventSource.java:60 id range)
+    price  = (r(i,3) >> 11) * 2^-53  in [0, 1)  (Random.nextDouble, :61)
+    ts     = T0 + floor(i / R) ms
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 0x5EEDC0DE
+GOLDEN = 0x9E3779B97F4A7C15
+T0 = 1_500_000_000_000
+
+PATTERN_PLAN = (
+    "define stream A (k int, ts long, id int, price double);"
+    "define stream B (k int, ts long, id int, price double);"
+    "partition with (k of A, k of B) begin "
+    "from every s1=A[price > 0.5] -> s2=B[id % 7 == 0] within 10 sec "
+    "select s1.k as k, s1.price as p1, s2.price as p2, s2.ts as t "
+    "insert into O; end;")
+
+FILTER_PLAN = (
+    "define stream inputStream (id int, name string, price double, timestamp long);"
+    "from inputStream[price > 0.5 and id % 7 == 0] select * insert into O;")
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(GOLDEN)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def generate(first: int, n: int, keys: int, rate: int = 400, seed: int = SEED,
+             t0: int = T0, single_stream: bool = False):
+    """Columns for events [first, first+n): dict of numpy arrays."""
+    i = np.arange(first, first + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        b = np.uint64(seed) ^ (i * np.uint64(GOLDEN))
+    key = (splitmix64(b ^ np.uint64(0)) % np.uint64(keys)).astype(np.int32)
+    stream = np.zeros(n, np.uint8) if single_stream else \
+        (splitmix64(b ^ np.uint64(1)) >> np.uint64(63)).astype(np.uint8)
+    idv = (splitmix64(b ^ np.uint64(2)) % np.uint64(50)).astype(np.int32)
+    price = (splitmix64(b ^ np.uint64(3)) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    ts = (t0 + (i // np.uint64(rate)).astype(np.int64)).astype(np.int64)
+    return {"k": key, "stream": stream, "id": idv, "price": price, "ts": ts}
+
+
+def generate_device(first: int, n: int, keys: int, rate: int = 400, seed: int = SEED,
+                    t0: int = T0, single_stream: bool = False, device="cuda"):
+    """Same stream, generated on the GPU into torch tensors (bench inputs)."""
+    import ctypes as C
+    import torch
+    from . import _lib as L
+    key = torch.empty(n, dtype=torch.int32, device=device)
+    ts = torch.empty(n, dtype=torch.int64, device=device)
+    stream = torch.empty(n, dtype=torch.uint8, device=device)
+    idv = torch.empty(n, dtype=torch.int32, device=device)
+    price = torch.empty(n, dtype=torch.float64, device=device)
+    s = torch.cuda.current_stream(device).cuda_stream
+    rc = L.lib().cep_generate(first, n, seed, keys, rate, t0, 1 if single_stream else 0,
+                              C.c_void_p(key.data_ptr()), C.c_void_p(ts.data_ptr()),
+                              C.c_void_p(stream.data_ptr()), C.c_void_p(idv.data_ptr()),
+                              C.c_void_p(price.data_ptr()), C.c_void_p(s))
+    L.raise_for(rc, "cep_generate failed")
+    return {"k": key, "stream": stream, "id": idv, "price": price, "ts": ts}

@@ -1,0 +1,227 @@
+/*
+ * libcep — MI355X-native complex-event-matching engine, C ABI.
+ *
+ * Drop-in boundary for the Siddhi runtime calls that flink-siddhi's
+ * operator makes.  Every reference path below is relative to
+ * core/src/main/java/org/apache/flink/streaming/siddhi/ in tammypi/flink-siddhi.
+ * Plain C types only: pointers, sizes, status codes.  A JNI or Panama binding
+ *  maps status codes onto the reference's exceptions.
+ *
+ * Threading: one cep_app per (Flink subtask, execution plan), as one
+ * QueryRuntimeHandler per plan (operator/AbstractSiddhiOperator.java:114-176).
+ * All calls come from one thread.  Matches are delivered through the output
+ * callback on the calling thread, inside cep_flush(), before it returns —
+ * the analogue of StreamCallback.receive(Event[]) running synchronously in
+ * InputHandler.send (operator/StreamOutputHandler.java:63).
+ *
+ * Ownership: input buffers stay owned by the caller and are consumed before
+ * cep_send_batch() returns.  Output rows handed to the callback are owned by
+ * the engine and valid only during the callback.  Snapshot buffers are
+ * engine-allocated and released with cep_free().
+ */
+#ifndef CEP_H_
+#define CEP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------
+ * Mapping used by the Java shim:
+ *   CEP_E_PARSE            -> SiddhiAppCreationException (fail-fast at DAG
+ *                             build, AbstractSiddhiOperator.java:292-299)
+ *   CEP_E_UNDEFINED_STREAM -> exception/UndefinedStreamException.java:20
+ *                             (thrown at AbstractSiddhiOperator.java:205,
+ *                              SiddhiOperatorContext.java:151)
+ *   CEP_E_DUPLICATED_STREAM-> exception/DuplicatedStreamException.java:20
+ *   CEP_E_UNSUPPORTED      -> valid SiddhiQL outside the engine subset
+ *                             (joins, windows, tables): shim falls back to
+ *                             real Siddhi
+ *   CEP_E_ARG              -> IllegalArgumentException
+ *                             (operator/StreamOutputHandler.java:89)
+ *   CEP_E_DEVICE           -> HIP failure / no gfx950 device
+ *   CEP_E_CAPACITY         -> per-key pending-state or key-space capacity
+ *                             exceeded (raise cep_options.pending_slots /
+ *                             key_capacity)
+ *   CEP_E_STATE            -> snapshot incompatible with this plan
+ */
+enum {
+  CEP_OK = 0,
+  CEP_E_PARSE = 1,
+  CEP_E_UNDEFINED_STREAM = 2,
+  CEP_E_DUPLICATED_STREAM = 3,
+  CEP_E_UNSUPPORTED = 4,
+  CEP_E_ARG = 5,
+  CEP_E_DEVICE = 6,
+  CEP_E_CAPACITY = 7,
+  CEP_E_STATE = 8
+};
+
+/* Attribute types: the Siddhi attribute types of utils/SiddhiTypeFactory.java:42-54
+ * (STRING, INT, LONG, FLOAT, DOUBLE, BOOL; anything else OBJECT).
+ * Column element layouts: INT int32, LONG int64, FLOAT float, DOUBLE double,
+ * BOOL uint8 (0/1), STRING int32 dictionary id (cep_dict_intern). */
+typedef enum {
+  CEP_INT = 0, CEP_LONG = 1, CEP_FLOAT = 2, CEP_DOUBLE = 3, CEP_BOOL = 4,
+  CEP_STRING = 5, CEP_OBJECT = 6
+} cep_type;
+
+typedef struct {
+  char name[64];
+  int32_t type;
+} cep_attr;
+
+typedef struct cep_options {
+  int32_t device;          /* HIP device ordinal (default 0) */
+  int32_t pending_slots;   /* per-key pending partial matches (default 16) */
+  int64_t key_capacity;    /* partition / group keys are ints in [0, key_capacity) (default 1<<20) */
+  int64_t chunk_events;    /* events per device chunk (default 1<<22) */
+  int32_t buckets_log2;    /* key buckets per chunk, log2 (default 10) */
+  int32_t profile;         /* 1: time every kernel with HIP events (cep_stats) */
+  int32_t ordered_output;  /* 1: deliver matches in Siddhi's global emission
+                              order; 0: per-key order (default 1) */
+  int32_t key_stride;      /* multi-GPU: this shard owns keys with key % key_stride == key_offset (default 1/0) */
+  int32_t key_offset;
+  int32_t reserved[7];
+} cep_options;
+
+/* Fill *opt with defaults. */
+void cep_default_options(cep_options* opt);
+
+typedef struct cep_app cep_app;
+
+/* A columnar batch of input events in arrival order.  `cols` follow the
+ * attribute order of the stream definition (schema/StreamSchema.java:89-149,
+ * the row order of schema/StreamSerializer.java:38-66).  A batch mixing
+ * several input streams (per-row `stream` handles) requires identical
+ * definitions for those streams. */
+typedef struct {
+  int64_t n;
+  const int64_t* ts;          /* event timestamps, ms (InputHandler.send(ts, row)) */
+  const uint8_t* stream;      /* per-row input handle, or NULL: all rows are `input` */
+  int32_t input;              /* input handle (cep_input) when stream == NULL */
+  int32_t ncols;
+  const void* const* cols;    /* ncols column pointers */
+  int32_t on_device;          /* 1: ts/stream/cols are device pointers */
+} cep_batch;
+
+/* Output rows, columnar, in emission order (see cep_options.ordered_output). */
+typedef struct {
+  const char* stream_id;
+  int64_t n;
+  int32_t ncols;
+  const int64_t* ts;          /* output event timestamps (completing event) */
+  const int64_t* seq;         /* arrival sequence number of the completing event */
+  const void* const* cols;
+} cep_rows;
+
+typedef void (*cep_emit_fn)(void* user, const cep_rows* rows);
+
+typedef struct {
+  int64_t events_in;
+  int64_t matches_out;
+  int64_t batches;
+  int64_t kernel_launches[8];
+  double kernel_ms[8];        /* with cep_options.profile: summed HIP-event time */
+} cep_stats_t;
+
+/* Kernel kinds indexing cep_stats_t arrays. */
+enum {
+  CEP_K_FILTER = 0, CEP_K_PARTITION = 1, CEP_K_WALK = 2, CEP_K_ROUTE = 3,
+  CEP_K_ORDER = 4, CEP_K_AGG = 5, CEP_K_OTHER = 6
+};
+
+/* ---- plan-level calls (no device needed) ------------------------------ */
+
+/* SiddhiManager.validateSiddhiApp(plan)  — AbstractSiddhiOperator.java:295 */
+int cep_validate(const char* plan, char* err, size_t errlen);
+
+/* SiddhiTypeFactory.getStreamDefinition(plan, streamId) — utils/SiddhiTypeFactory.java:64-84
+ * (the throw-away runtime used by returns(...) to infer output TypeInfo). */
+int cep_plan_schema(const char* plan, const char* stream_id, cep_attr* out,
+                    int cap, int* n, char* err, size_t errlen);
+
+/* ---- runtime ----------------------------------------------------------- */
+
+/* SiddhiManager.createSiddhiAppRuntime(plan) + start()
+ * — AbstractSiddhiOperator.java:120-122,137-142.  NULL on error. */
+cep_app* cep_create(const char* plan, const cep_options* opt, char* err,
+                    size_t errlen);
+
+/* SiddhiAppRuntime.shutdown() — AbstractSiddhiOperator.java:144-148 */
+void cep_destroy(cep_app* app);
+
+/* getStreamDefinitionMap().get(id) — AbstractSiddhiOperator.java:160-163 */
+int cep_stream_schema(cep_app* app, const char* stream_id, cep_attr* out,
+                      int cap, int* n);
+
+/* getInputHandler(id) — AbstractSiddhiOperator.java:172.
+ * Returns a handle >= 0, or -CEP_E_UNDEFINED_STREAM. */
+int cep_input(cep_app* app, const char* stream_id);
+
+/* addCallback(outId, StreamCallback) — AbstractSiddhiOperator.java:165-166 */
+int cep_set_callback(cep_app* app, const char* out_id, cep_emit_fn fn,
+                     void* user);
+
+/* A batch of InputHandler.send(ts, row) calls — AbstractSiddhiOperator.java:130 */
+int cep_send_batch(cep_app* app, const cep_batch* batch);
+
+/* Deliver every match of the input sent so far to the callbacks; called
+ * before emitWatermark / snapshotState / close (AbstractSiddhiOperator.java:246,331,316). */
+int cep_flush(cep_app* app);
+
+/* Device-resident consumers: expose the current (unflushed) output rows of
+ * out_id as device pointers, valid until the next send/flush/reset. */
+int cep_output_device(cep_app* app, const char* out_id, cep_rows* rows);
+
+/* Drop unflushed outputs (device-resident consumers after reading them). */
+int cep_reset_output(cep_app* app);
+
+/* SiddhiAppRuntime.snapshot() — AbstractSiddhiOperator.java:374-380.
+ * Restore is a TODO in the reference (AbstractSiddhiOperator.java:341);
+ * cep_restore makes it real. */
+int cep_snapshot(cep_app* app, uint8_t** buf, size_t* len);
+int cep_restore(cep_app* app, const uint8_t* buf, size_t len);
+void cep_free(void* p);
+
+/* QueryRuntimeHandler.enable()/disable() — AbstractSiddhiOperator.java:150-156,
+ * events sent while disabled are dropped (:128). */
+int cep_set_enabled(cep_app* app, int enabled);
+
+/* String dictionary (STRING columns carry int32 ids). */
+int32_t cep_dict_intern(cep_app* app, const char* s);
+const char* cep_dict_lookup(cep_app* app, int32_t id);
+
+int cep_stats(cep_app* app, cep_stats_t* out);
+const char* cep_last_error(cep_app* app);
+
+/* ---- multi-GPU key shuffle (Flink keyBy / router/DynamicPartitioner.java:43-60,
+ * router/HashPartitioner.java:24-26) -------------------------------------
+ * cep_route_batch evaluates the predicates of the app's (single) keyed
+ * pattern over a device batch and writes the relevant events as fixed-size
+ * records grouped by owner shard (key % world): records for shard r land in
+ * rec_out[offsets[r] .. offsets[r]+counts[r]) in arrival order.  The caller
+ * exchanges them (RCCL all-to-all) and feeds the received records, in
+ * source-rank order, to the owner's app with cep_send_records. */
+int cep_record_words(cep_app* app);               /* 8-byte words per record */
+int cep_route_batch(cep_app* app, const cep_batch* batch, int world,
+                    void* rec_out, int64_t rec_cap, int64_t* counts_host);
+int cep_send_records(cep_app* app, const void* recs, int64_t n,
+                     int64_t events_represented);
+
+/* Synthetic workload generator (bench / tests only — BASELINE.md §3):
+ * r(i,j) = splitmix64(seed ^ (i*0x9E3779B97F4A7C15) ^ j); key = r(i,0) mod K;
+ * stream = r(i,1)>>63 (0 = A, 1 = B, or 0 when single_stream); id = r(i,2) mod 50;
+ * price = (r(i,3)>>11) * 2^-53; ts = t0 + floor(i / rate).  Device pointers. */
+int cep_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
+                 int64_t rate, int64_t t0, int single_stream, int32_t* key,
+                 int64_t* ts, uint8_t* stream, int32_t* id, double* price,
+                 void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CEP_H_ */
