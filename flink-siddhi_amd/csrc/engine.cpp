@@ -79,6 +79,8 @@ struct PatternRT {
   DevBuf recs, tile_off;
   int64_t chunk = 0;
   int64_t extra_bound = 0;   // pending partials that may still complete
+  bool part_vm = true;       // partition pass needs the interpreter
+  bool walk_vm = true;       // walk needs the interpreter (g on s1, computed select items)
 };
 
 struct TimedLaunch {
@@ -185,6 +187,7 @@ OutArgs out_args(OutStream& o, const Query& q) {
     oa.col[c] = o.cols[c].p;
     oa.type[c] = o.types[c];
     oa.prog[c] = q.select[c].prog.off;
+    oa.src[c] = q.select[c].src;
   }
   oa.ts = (int64_t*)o.ts.p;
   oa.seq = (int64_t*)o.seq.p;
@@ -239,7 +242,10 @@ int create_runtime(cep_app* a) {
     p.f_prog = q.f.off;
     p.g_raw_prog = q.g_raw.off;
     p.g_walk_prog = q.g_walk.off;
+    p.f_terms = q.f_terms;
+    p.g_terms = q.g_terms;
     p.every = q.every ? 1 : 0;
+    p.closed_form = (q.every && !q.g_in_walk) ? 1 : 0;
     p.within = q.within;
     p.key_col_a = q.key_col_a;
     p.key_col_b = q.key_col_b;
@@ -282,6 +288,9 @@ int create_runtime(cep_app* a) {
         !dev_ensure(&rt.tile_off, (size_t)ntiles * ((1 << lg) + 1) * 2, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
     rt.extra_bound = (int64_t)S * kc;
+    rt.part_vm = (q.f.off >= 0 && q.f_terms.n < 0) || (q.g_raw.off >= 0 && q.g_terms.n < 0);
+    rt.walk_vm = q.g_in_walk;
+    for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
     a->pats.push_back(rt);
   }
   hipStreamSynchronize(a->stream);
@@ -324,12 +333,15 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
   fa.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
   fa.in_stream = q.in_stream;
   fa.filter_prog = q.filter.off;
+  fa.filter_terms = q.filter_terms;
   fa.out = out_args(o, q);
   fa.tile_state = (unsigned long long*)a->tile_state.p;
   fa.ticket = (unsigned int*)a->ticket.p;
   fa.err = (unsigned int*)a->err.p;
   LaunchTimer t(a, CEP_K_FILTER);
-  launch_filter(fa, ntiles, a->stream);
+  bool vm = q.filter.off >= 0 && q.filter_terms.n < 0;
+  for (auto& it : q.select) vm |= it.src < SRC_REC || it.src >= SRC_TS;
+  launch_filter(fa, ntiles, vm, a->stream);
   return CEP_OK;
 }
 
@@ -358,7 +370,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     pa.err = (unsigned int*)a->err.p;
     {
       LaunchTimer t(a, CEP_K_PARTITION);
-      launch_partition(pa, ntiles, a->stream);
+      launch_partition(pa, ntiles, rt.part_vm, a->stream);
     }
     WalkArgs wa{};
     wa.vm = pa.vm;
@@ -368,6 +380,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     wa.ntiles = (int)ntiles;
     wa.tile_rows = pa.tile_rows;
     wa.seq_chunk0 = rows.seq0 + rows.row0;
+    wa.ts_base = rows.ts + rows.row0;
     wa.pcnt = (uint8_t*)rt.pcnt.p;
     wa.started = (uint8_t*)rt.started.p;
     wa.slots = (uint64_t*)rt.slots.p;
@@ -375,7 +388,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     wa.err = pa.err;
     {
       LaunchTimer t(a, CEP_K_WALK);
-      launch_walk(wa, P, a->stream);
+      launch_walk(wa, P, rt.walk_vm, a->stream);
     }
   }
   return CEP_OK;

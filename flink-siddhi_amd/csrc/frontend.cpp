@@ -887,6 +887,142 @@ class CodeGen {
   }
 };
 
+// ---- interpreter-free predicate lowering (plan.h TermList) ----------------
+uint64_t host_convert(uint64_t v, int from, int to) {
+  if (from == to || to == T_LONG) return v;
+  if (to == T_FLOAT) {
+    float f = from == T_INT ? (float)(int32_t)v : from == T_LONG ? (float)(int64_t)v : 0.f;
+    if (from == T_FLOAT) return v;
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+  }
+  if (to == T_DOUBLE) {
+    double d;
+    if (from == T_INT) d = (double)(int32_t)v;
+    else if (from == T_LONG) d = (double)(int64_t)v;
+    else if (from == T_FLOAT) {
+      float f;
+      uint32_t u = (uint32_t)v;
+      std::memcpy(&f, &u, 4);
+      d = f;
+    } else return v;
+    uint64_t r;
+    std::memcpy(&r, &d, 8);
+    return r;
+  }
+  return v;
+}
+
+uint8_t cmp_op(const std::string& op, bool flip) {
+  if (op == "==") return OP_EQ;
+  if (op == "!=") return OP_NE;
+  if (op == "<") return flip ? OP_GT : OP_LT;
+  if (op == "<=") return flip ? OP_GE : OP_LE;
+  if (op == ">") return flip ? OP_LT : OP_GT;
+  return flip ? OP_LE : OP_GE;
+}
+
+uint8_t arith_op(const std::string& op) {
+  if (op == "+") return OP_ADD;
+  if (op == "-") return OP_SUB;
+  if (op == "*") return OP_MUL;
+  if (op == "/") return OP_DIV;
+  if (op == "%") return OP_MOD;
+  return 0;
+}
+
+bool is_col(const ExprP& e) { return e->k == Expr::ATTR && e->col >= 0 && e->out < 0; }
+
+bool lower_atom(const ExprP& e, Term* t) {
+  ExprP lhs, rhs;
+  bool flip = false;
+  if (e->k == Expr::ATTR && e->t == T_BOOL && is_col(e)) {   // `[flag]`
+    t->col = e->col; t->coltype = T_BOOL; t->aop = 0; t->atype = T_BOOL; t->aconst = 0;
+    t->cop = OP_EQ; t->ctype = T_INT; t->cconst = 1;
+    return true;
+  }
+  if (e->k != Expr::BIN) return false;
+  const std::string& op = e->op;
+  if (!(op == "==" || op == "!=" || op == "<" || op == "<=" || op == ">" || op == ">=")) return false;
+  if (e->args[1]->k == Expr::CONST) { lhs = e->args[0]; rhs = e->args[1]; }
+  else if (e->args[0]->k == Expr::CONST) { lhs = e->args[1]; rhs = e->args[0]; flip = true; }
+  else return false;
+  ExprP col;
+  int aop = 0;
+  ExprP ak;
+  if (is_col(lhs)) col = lhs;
+  else if (lhs->k == Expr::BIN && arith_op(lhs->op) && is_col(lhs->args[0]) &&
+           lhs->args[1]->k == Expr::CONST) {
+    col = lhs->args[0];
+    aop = arith_op(lhs->op);
+    ak = lhs->args[1];
+  } else return false;
+  t->col = col->col;
+  t->coltype = col->t;
+  t->aop = aop;
+  if (aop) {
+    t->atype = promote(col->t, ak->t);
+    t->aconst = host_convert(ak->bits, ak->t, t->atype);
+  } else {
+    t->atype = col->t;
+    t->aconst = 0;
+  }
+  const int at = aop ? t->atype : col->t;
+  if (numeric(at) && numeric(rhs->t)) {
+    t->ctype = promote(at, rhs->t);
+  } else if (at == rhs->t && (at == T_STRING || at == T_BOOL)) {
+    t->ctype = T_INT;
+  } else {
+    return false;
+  }
+  t->cconst = numeric(rhs->t) ? host_convert(rhs->bits, rhs->t, t->ctype) : rhs->bits;
+  t->cop = cmp_op(op, flip);
+  return true;
+}
+
+void flatten(const ExprP& e, const std::string& op, std::vector<ExprP>* out) {
+  if (e->k == Expr::BIN && e->op == op) {
+    flatten(e->args[0], op, out);
+    flatten(e->args[1], op, out);
+  } else {
+    out->push_back(e);
+  }
+}
+
+TermList lower_terms(const std::vector<ExprP>& conj) {
+  TermList tl;
+  if (conj.empty()) return tl;
+  std::vector<ExprP> atoms;
+  for (auto& c : conj) flatten(c, "and", &atoms);
+  bool any = false;
+  if (atoms.size() == 1 && atoms[0]->k == Expr::BIN && atoms[0]->op == "or") {
+    std::vector<ExprP> ors;
+    flatten(atoms[0], "or", &ors);
+    atoms = ors;
+    any = true;
+  }
+  if ((int)atoms.size() > kMaxTerms) return tl;
+  TermList r;
+  r.any = any ? 1 : 0;
+  r.n = 0;
+  for (auto& a : atoms) {
+    if (!lower_atom(a, &r.t[r.n])) return tl;
+    ++r.n;
+  }
+  return r;
+}
+
+// Plain attribute copies bypass the VM in the output projection.
+int32_t direct_source(const CompiledApp* app, const Prog& p) {
+  if (p.len != 2) return SRC_VM;
+  const Ins& in = app->code[p.off];
+  if (app->code[p.off + 1].op != OP_END || in.dst != 0) return SRC_VM;
+  if (in.op == OP_LDCAP) return SRC_CAP + (int32_t)in.imm;
+  if (in.op == OP_LDCOL) return SRC_REC + (int32_t)in.imm;
+  return SRC_VM;
+}
+
 Prog compile_and(CompiledApp* app, const std::vector<ExprP>& es, const Loader& ld) {
   if (es.empty()) return Prog{};
   ExprP acc = es[0];
@@ -947,6 +1083,7 @@ void compile_single(CompiledApp* app, QueryAst& q) {
   }
   Loader raw{[](const Expr& e) { return std::make_pair((uint8_t)OP_LDCOL, (uint32_t)e.col); }};
   out.filter = compile_and(app, q.filters, raw);
+  out.filter_terms = lower_terms(q.filters);
   if (q.select_all) {
     q.select.clear();
     for (auto& a : sd.attrs) {
@@ -975,6 +1112,7 @@ void compile_single(CompiledApp* app, QueryAst& q) {
     oi.type = it.e->t;
     if (oi.type == T_OBJECT) fail(CEP_E_UNSUPPORTED, "object attributes in select");
     oi.prog = cg.compile(it.e);
+    oi.src = direct_source(app, oi.prog);   // SRC_REC + c = input column c
     out.select.push_back(oi);
   }
   for (auto& call : calls) {
@@ -1125,6 +1263,7 @@ void compile_pattern(CompiledApp* app, QueryAst& q) {
   if (q.states[0].cond) {
     CodeGen cg(app, raw);
     out.f = cg.compile(q.states[0].cond);
+    out.f_terms = lower_terms({q.states[0].cond});
   }
   Query* op = &out;
   Loader walk{[op, &cap_a](const Expr& e) {
@@ -1141,8 +1280,12 @@ void compile_pattern(CompiledApp* app, QueryAst& q) {
   }};
   if (q.states[1].cond) {
     CodeGen cg(app, out.g_in_walk ? walk : raw);
-    if (out.g_in_walk) out.g_walk = cg.compile(q.states[1].cond);
-    else out.g_raw = cg.compile(q.states[1].cond);
+    if (out.g_in_walk) {
+      out.g_walk = cg.compile(q.states[1].cond);
+    } else {
+      out.g_raw = cg.compile(q.states[1].cond);
+      out.g_terms = lower_terms({q.states[1].cond});
+    }
   }
   for (auto& it : q.select) {
     CodeGen cg(app, walk);
@@ -1150,6 +1293,7 @@ void compile_pattern(CompiledApp* app, QueryAst& q) {
     oi.name = it.name;
     oi.type = it.e->t;
     oi.prog = cg.compile(it.e);
+    oi.src = direct_source(app, oi.prog);   // SRC_CAP + i = s1 capture, SRC_REC + i = s2 word
     out.select.push_back(oi);
   }
   if (q.partitioned) {

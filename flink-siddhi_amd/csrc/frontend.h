@@ -46,6 +46,7 @@ struct OutItem {
   std::string name;
   int type;
   Prog prog;
+  int32_t src = SRC_VM;          // direct copy source when the item is a plain attribute
 };
 
 struct Query {
@@ -57,6 +58,7 @@ struct Query {
   // ---- filter / aggregation (single input stream)
   int in_stream = -1;
   Prog filter;                   // conjunction of all [..] filters, invalid = true
+  TermList filter_terms;
   int key_col = -1;              // partition / group key column (-1: none)
   int part_col = -1;             // `partition with` column (-1: none)
   std::vector<Prog> group_progs; // group-by expressions (host path when not a column)
@@ -66,6 +68,7 @@ struct Query {
   int a_stream = -1, b_stream = -1;
   Prog f;                        // over A's columns (LDCOL = raw column)
   Prog g_raw;                    // g over B's raw columns (valid iff !g_in_walk)
+  TermList f_terms, g_terms;     // interpreter-free forms of f / g_raw
   Prog g_walk;                   // g in the walk: LDCOL = record word, LDCAP = s1 capture
   bool g_in_walk = false;
   bool every = false;

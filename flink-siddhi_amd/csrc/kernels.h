@@ -39,6 +39,7 @@ struct OutArgs {
   void* col[kMaxOut];
   int32_t type[kMaxOut];
   int32_t prog[kMaxOut];   // program offset per output attribute
+  int32_t src[kMaxOut];    // SRC_* direct source, or SRC_VM
   int32_t ncols;
   int64_t* ts;
   int64_t* seq;
@@ -61,6 +62,7 @@ struct FilterArgs {
   VmArgs vm;
   int32_t in_stream;
   int32_t filter_prog;     // -1: no filter
+  TermList filter_terms;   // n >= 0: interpreter-free form of the filter
   OutArgs out;
   unsigned long long* tile_state;   // decoupled look-back words (zeroed per launch)
   unsigned int* ticket;             // tile ticket counter (zeroed per launch)
@@ -73,6 +75,7 @@ struct PatternArgs {
   int32_t a_stream, b_stream;
   int32_t f_prog;          // -1: true
   int32_t g_raw_prog;      // g evaluated in the partition pass (-1: true / in walk)
+  TermList f_terms, g_terms;   // n >= 0: interpreter-free f / g_raw
   int32_t g_walk_prog;     // g evaluated per (pending, B) in the walk (-1: none)
   int32_t every;
   int64_t within;          // -1: none
@@ -87,6 +90,7 @@ struct PatternArgs {
   int64_t key_capacity;    // dense keys per shard
   int32_t key_stride, key_offset;   // shard ownership (key % stride == offset)
   int32_t buckets_log2;
+  int32_t closed_form;     // 1: every && g independent of s1 -> data-parallel walk
 };
 
 struct PartArgs {
@@ -110,6 +114,7 @@ struct WalkArgs {
   int32_t ntiles;
   int32_t tile_rows;
   int64_t seq_chunk0;          // sequence number of the chunk's first row
+  const int64_t* ts_base;      // device: ts of the chunk's first row (closed form)
   // per-key state (global, dense key index)
   uint8_t* pcnt;
   uint8_t* started;
@@ -119,9 +124,9 @@ struct WalkArgs {
 };
 
 // --------------------------------------------------------------- launchers --
-void launch_filter(const FilterArgs& a, int64_t ntiles, hipStream_t s);
-void launch_partition(const PartArgs& a, int64_t ntiles, hipStream_t s);
-void launch_walk(const WalkArgs& a, int nbuckets, hipStream_t s);
+void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
+void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
+void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s);
 void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
                      int64_t rate, int64_t t0, int single_stream, int32_t* key,
                      int64_t* ts, uint8_t* stream, int32_t* id, double* price,

@@ -2,10 +2,9 @@
 // AbstractSiddhiOperator.java:130 `InputHandler.send(ts, row)`):
 //
 //   k_filter     `from S[expr] select ... insert into O`: columnar predicate
-//                evaluation + order-preserving compaction (64-bit wave ballot,
-//                mbcnt ranks, single-pass decoupled look-back across tiles) +
-//                projection.  HBM-bound: reads the predicate columns once,
-//                writes the selected rows once.
+//                evaluation (16 consecutive rows per lane, 16-byte loads) +
+//                order-preserving compaction (block scan + single-pass
+//                decoupled look-back across tiles) + projection.
 //   k_partition  keyed pattern, pass 1: evaluates the state filters f / g on
 //                the event columns, drops events no state can use (exact for
 //                `->` patterns) and scatters the rest as
@@ -13,10 +12,13 @@
 //                (LDS histogram + LDS scan; no global atomics).
 //   k_walk       keyed pattern, pass 2: one workgroup per key bucket gathers
 //                its segments (tile order = arrival order), groups them by
-//                key in LDS, and runs one NFA lane per key: `within` pruning,
-//                completion of pending partials in creation order, `every`
-//                re-arming.  Matches are reserved with one atomic per window
-//                and projected in place.
+//                key in LDS and resolves the pattern:
+//                  closed form (`every`, g independent of s1, SURVEY.md
+//                  App. A.3): every A matches the next B of its key within W
+//                  -> segmented next-B scan, per-record match flags, one block
+//                  scan for output positions; fully data-parallel;
+//                  general form: one NFA lane per key walking its records
+//                  (count pass + emit pass), pending partials in LDS lists.
 //   k_generate   counter-based synthetic workload.
 #include <hip/hip_runtime.h>
 
@@ -29,19 +31,13 @@ namespace {
 
 constexpr uint64_t kStatusShift = 62;
 constexpr uint64_t kValueMask = (1ull << 62) - 1;
-
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
-
-__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
+constexpr uint16_t kNone16 = 0xffff;
 
 __device__ __forceinline__ void set_err(unsigned int* err, unsigned int bit) {
   if (err) atomicOr(err, bit);
 }
 
-// Block-wide exclusive scan of one value per thread (256 threads).
+// Block-wide exclusive scan of one value per thread (blockDim = 256).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch /*>=5*/,
                                                     uint32_t* total) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -55,7 +51,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
   __syncthreads();
   if (tid == 0) {
     uint32_t s = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+    for (int w = 0; w < 4; ++w) {
       uint32_t t = scratch[w];
       scratch[w] = s;
       s += t;
@@ -87,48 +83,133 @@ __device__ __forceinline__ bool eval_pred(const VmArgs& vm, int prog, uint64_t* 
   return !isnull && (v & 1u);
 }
 
+__device__ __forceinline__ uint64_t eval_word(const VmArgs& vm, int prog, uint64_t* R,
+                                                        const RowEnv& env) {
+  bool isnull = false;
+  uint64_t v = vm_eval(vm.code, vm.konst, prog, R, threadIdx.x, blockDim.x, env, &isnull);
+  return isnull ? 0 : v;
+}
+
+// Load N consecutive elements [row, row + N) of a typed column as VM words,
+// with 16-byte vector loads when the run is full and aligned.
+template <int N>
+__device__ __forceinline__ void load_run(const void* p, int type, int64_t row, int64_t nvalid,
+                                         uint64_t (&v)[N]) {
+  const int w = type_width(type);
+  const uintptr_t addr = (uintptr_t)p + (uintptr_t)(row * w);
+  if (nvalid >= N && (addr & 15u) == 0 && (w * N) % 16 == 0) {
+    if (w == 8) {
+#pragma unroll
+      for (int i = 0; i < N / 2; ++i) {
+        const uint4 x = gload4((const void*)(addr + 16 * i));
+        v[2 * i] = ((uint64_t)x.y << 32) | x.x;
+        v[2 * i + 1] = ((uint64_t)x.w << 32) | x.z;
+      }
+    } else if (w == 4) {
+#pragma unroll
+      for (int i = 0; i < N / 4; ++i) {
+        const uint4 x = gload4((const void*)(addr + 16 * i));
+        const uint32_t e[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[4 * i + j] = type == T_FLOAT ? (uint64_t)e[j] : from_i32((int32_t)e[j]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < N / 16; ++i) {
+        const uint4 x = gload4((const void*)(addr + 16 * i));
+        const uint32_t e[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          v[16 * i + j] = ((e[j >> 2] >> (8 * (j & 3))) & 0xffu) ? 1u : 0u;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = i < nvalid ? load_col(p, type, row + i) : 0;
+}
+
+// Interpreter-free predicate over N consecutive rows -> bit i set when row i
+// passes.  Stage-wise: one switch per stage, straight loops over the N values.
+template <int N>
+__device__ __forceinline__ uint32_t eval_terms_run(const TermList& tl, const RowsArgs& rows,
+                                                   int64_t row, int64_t nvalid) {
+  uint32_t acc = tl.any ? 0u : ((N >= 32) ? 0xffffffffu : ((1u << N) - 1u));
+  for (int i = 0; i < tl.n; ++i) {
+    const Term& t = tl.t[i];
+    uint64_t v[N];
+    load_run<N>(rows.cols.p[t.col], t.coltype, row, nvalid, v);
+    int ty = (t.coltype == T_BOOL || t.coltype == T_STRING) ? T_INT : t.coltype;
+    uint32_t nullm = 0;
+    if (t.aop) {
+      convert_run<N>(v, ty, t.atype);
+      arith_run<N>(v, t.aop, t.atype, t.aconst, &nullm);
+      ty = t.atype;
+    }
+    convert_run<N>(v, ty, t.ctype);
+    const uint32_t bits = compare_run<N>(v, t.cop, t.ctype, t.cconst) & ~nullm;
+    acc = tl.any ? (acc | bits) : (acc & bits);
+  }
+  return acc;
+}
+
+// Predicate over N consecutive rows: term list when available, else the VM.
+template <int N, bool kVm>
+__device__ __forceinline__ uint32_t eval_run(const TermList& tl, const VmArgs& vm, int prog,
+                                             uint64_t* R, const RowsArgs& rows, int64_t row,
+                                             int64_t nvalid) {
+  const uint32_t full = (N >= 32) ? 0xffffffffu : ((1u << N) - 1u);
+  if (prog < 0) return full;
+  if (!kVm || tl.n >= 0) return eval_terms_run<N>(tl, rows, row, nvalid);
+  uint32_t bits = 0;
+  for (int e = 0; e < N; ++e)
+    if (e < nvalid && eval_pred(vm, prog, R, RowEnv{&rows, row + e})) bits |= 1u << e;
+  return bits;
+}
+
 }  // namespace
 
 // ============================================================== k_filter ==
+// kVm = false: filter and projection are TermList / direct copies (no interpreter).
+template <bool kVm>
 __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
   __shared__ uint64_t R[kMaxRegs * kFilterThreads];
-  __shared__ uint32_t cnt[kFilterItems * 4];
+  __shared__ uint32_t scratch[8];
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_prefix;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   constexpr int kTile = kFilterThreads * kFilterItems;
 
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t base = tile * kTile;
+  const int64_t r0 = tile * kTile + (int64_t)tid * kFilterItems;   // first row of this lane
+  const int64_t nvalid = a.rows.n - r0;
+  const int64_t row0 = a.rows.row0 + r0;
 
-  uint32_t selmask = 0;
-#pragma unroll 1
-  for (int e = 0; e < kFilterItems; ++e) {
-    const int64_t r = base + (int64_t)e * kFilterThreads + tid;
-    bool sel = false;
-    if (r < a.rows.n) {
-      const int64_t row = a.rows.row0 + r;
-      const int s = a.rows.stream ? (int)a.rows.stream[row] : a.rows.input;
-      if (s == a.in_stream) sel = eval_pred(a.vm, a.filter_prog, R, RowEnv{&a.rows, row});
+  uint32_t sel = 0;
+  if (nvalid > 0) {
+    uint32_t in_stream = (1u << kFilterItems) - 1u;
+    if (a.rows.stream) {
+      in_stream = 0;
+#pragma unroll
+      for (int e = 0; e < kFilterItems; ++e)
+        if (e < nvalid && (int)a.rows.stream[row0 + e] == a.in_stream) in_stream |= 1u << e;
+    } else if (a.rows.input != a.in_stream) {
+      in_stream = 0;
     }
-    const uint64_t bal = __ballot(sel);
-    if (lane == 0) cnt[e * 4 + wave] = (uint32_t)__popcll(bal);
-    selmask |= (sel ? 1u : 0u) << e;
+    if (in_stream)
+      sel = in_stream & eval_run<kFilterItems, kVm>(a.filter_terms, a.vm, a.filter_prog, R, a.rows,
+                                               row0, nvalid);
+    if (nvalid < kFilterItems) sel &= (1u << nvalid) - 1u;
   }
-  __syncthreads();
-  // exclusive scan over (item, wave) in row order
+  uint32_t total;
+  const uint32_t mine = (uint32_t)__popc(sel);
+  const uint32_t off = block_excl_scan(mine, scratch, &total);
+
   if (tid == 0) {
-    uint32_t s = 0;
-    for (int i = 0; i < kFilterItems * 4; ++i) {
-      uint32_t t = cnt[i];
-      cnt[i] = s;
-      s += t;
-    }
-    const unsigned long long total = s;
     unsigned long long* flags = a.tile_state;
-    // publish the aggregate, then look back for the exclusive prefix
     unsigned long long prefix = 0;
     if (tile == 0) {
       prefix = __hip_atomic_load(a.out.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -163,30 +244,33 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
                          __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  const unsigned long long prefix = s_prefix;
-#pragma unroll 1
-  for (int e = 0; e < kFilterItems; ++e) {
-    const bool sel = (selmask >> e) & 1u;
-    const uint64_t bal = __ballot(sel);
-    if (!sel) continue;
-    const int64_t r = base + (int64_t)e * kFilterThreads + tid;
-    const int64_t row = a.rows.row0 + r;
-    const int64_t pos = (int64_t)prefix + cnt[e * 4 + wave] + mbcnt(bal);
-    if (pos >= a.out.cap) continue;
-    RowEnv env{&a.rows, row};
-    for (int c = 0; c < a.out.ncols; ++c) {
-      bool isnull = false;
-      uint64_t v = vm_eval(a.vm.code, a.vm.konst, a.out.prog[c], R, tid, kFilterThreads, env,
-                           &isnull);
-      store_col(a.out.col[c], a.out.type[c], pos, isnull ? 0 : v);
+  int64_t pos = (int64_t)s_prefix + off;
+  while (sel) {
+    const int e = __ffs(sel) - 1;
+    sel &= sel - 1;
+    const int64_t row = row0 + e;
+    if (pos < a.out.cap) {
+      RowEnv env{&a.rows, row};
+      for (int c = 0; c < a.out.ncols; ++c) {
+        const int src = a.out.src[c];
+        uint64_t v;
+        if (!kVm || (src >= SRC_REC && src < SRC_TS)) {
+          v = load_col(a.rows.cols.p[src - SRC_REC], a.rows.cols.t[src - SRC_REC], row);
+        } else {
+          v = eval_word(a.vm, a.out.prog[c], R, env);
+        }
+        store_col(a.out.col[c], a.out.type[c], pos, v);
+      }
+      a.out.ts[pos] = a.rows.ts[row];
+      a.out.seq[pos] = a.rows.seq0 + row;
     }
-    a.out.ts[pos] = a.rows.ts[row];
-    a.out.seq[pos] = a.rows.seq0 + row;
+    ++pos;
   }
 }
 
-void launch_filter(const FilterArgs& a, int64_t ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_filter, dim3((unsigned)ntiles), dim3(kFilterThreads), 0, s, a);
+void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) {
+  if (vm) hipLaunchKernelGGL(k_filter<true>, dim3((unsigned)ntiles), dim3(kFilterThreads), 0, s, a);
+  else hipLaunchKernelGGL(k_filter<false>, dim3((unsigned)ntiles), dim3(kFilterThreads), 0, s, a);
 }
 
 // =========================================================== k_partition ==
@@ -194,6 +278,7 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, hipStream_t s) {
 //   w0 = dense key (low 32) | role << 32 | input handle << 40
 //   w1 = arrival sequence number,  w2 = event timestamp,
 //   w3.. = carried columns (rec_a for A-stream rows, rec_b for B-stream rows)
+template <bool kVm>
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   __shared__ uint64_t R[kMaxRegs * kPartThreads];
   __shared__ uint32_t hist[4096 + 1];
@@ -205,75 +290,124 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   for (int i = tid; i <= P; i += kPartThreads) hist[i] = 0;
   __syncthreads();
 
-  uint32_t packed[kPartItems];
-  const int64_t tbase = tile * (int64_t)a.tile_rows;
+  constexpr int E = kPartItems;
+  const int64_t r0 = tile * (int64_t)a.tile_rows + (int64_t)tid * E;   // first row of this lane
+  const int64_t nvalid = a.rows.n - r0;
+  uint32_t packed[E];
 #pragma unroll
-  for (int e = 0; e < kPartItems; ++e) {
-    packed[e] = 0xffffffffu;
-    const int64_t r = tbase + (int64_t)e * kPartThreads + tid;
-    if (r >= a.rows.n) continue;
-    uint32_t role = 0;
-    int s;
-    int64_t key = 0;
+  for (int e = 0; e < E; ++e) packed[e] = 0xffffffffu;
+
+  if (nvalid > 0) {
+    uint32_t role_a = 0, role_b = 0, role_g = 0;
+    int64_t key[E];
     if (a.from_records) {
-      const uint64_t* rec = a.in_recs + r * p.rec_words;
-      const uint64_t h = rec[0];
-      role = (uint32_t)(h >> 32) & 0xffu;
-      s = (int)(h >> 40) & 0xff;
-      key = (int64_t)(uint32_t)h;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        key[e] = 0;
+        if (e < nvalid) {
+          const uint64_t h = a.in_recs[(r0 + e) * p.rec_words];
+          const uint32_t role = (uint32_t)(h >> 32) & 0xffu;
+          role_a |= ((role & ROLE_A) ? 1u : 0u) << e;
+          role_b |= ((role & ROLE_B) ? 1u : 0u) << e;
+          role_g |= ((role & ROLE_G) ? 1u : 0u) << e;
+          key[e] = (int64_t)(uint32_t)h;
+        }
+      }
     } else {
-      const int64_t row = a.rows.row0 + r;
-      s = a.rows.stream ? (int)a.rows.stream[row] : a.rows.input;
-      if (p.within >= 0) {
-        const int64_t prev = row > 0 ? a.rows.ts[row - 1] : a.rows.prev_ts;
-        if (a.rows.ts[row] < prev) set_err(a.err, ERR_ORDER);
+      const int64_t row0 = a.rows.row0 + r0;
+      uint32_t is_a = 0, is_b = 0;
+      int sid[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        sid[e] = a.rows.stream ? (e < nvalid ? (int)a.rows.stream[row0 + e] : -1) : a.rows.input;
+        if (e < nvalid) {
+          is_a |= (sid[e] == p.a_stream ? 1u : 0u) << e;
+          is_b |= (sid[e] == p.b_stream ? 1u : 0u) << e;
+        }
       }
-      RowEnv env{&a.rows, row};
-      if (s == p.a_stream && eval_pred(a.vm, p.f_prog, R, env)) role |= ROLE_A;
-      if (s == p.b_stream) {
-        if (p.g_walk_prog >= 0) role |= ROLE_B;
-        else if (eval_pred(a.vm, p.g_raw_prog, R, env)) role |= ROLE_B | ROLE_G;
+      if (p.within >= 0) {   // event-time order check (`within` pruning relies on it)
+        uint64_t t[E];
+        load_run<E>(a.rows.ts, T_LONG, row0, nvalid, t);
+        int64_t prev = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
+        bool bad = false;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (e < nvalid) {
+            bad |= (int64_t)t[e] < prev;
+            prev = (int64_t)t[e];
+          }
+        }
+        if (bad) set_err(a.err, ERR_ORDER);
       }
-      if (role) {
-        const int kc = s == p.a_stream ? p.key_col_a : p.key_col_b;
-        if (kc >= 0) key = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row);
+      if (is_a) role_a = is_a & eval_run<E, kVm>(p.f_terms, a.vm, p.f_prog, R, a.rows, row0, nvalid);
+      if (is_b) {
+        if (p.g_walk_prog >= 0) {
+          role_b = is_b;
+        } else {
+          role_b = is_b & eval_run<E, kVm>(p.g_terms, a.vm, p.g_raw_prog, R, a.rows, row0, nvalid);
+          role_g = role_b;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) key[e] = 0;
+      if (role_a | role_b) {
+        if (p.key_col_a >= 0 && p.key_col_a == p.key_col_b) {
+          uint64_t k[E];
+          load_run<E>(a.rows.cols.p[p.key_col_a], a.rows.cols.t[p.key_col_a], row0, nvalid, k);
+#pragma unroll
+          for (int e = 0; e < E; ++e) key[e] = (int64_t)k[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            if (((role_a | role_b) >> e) & 1u) {
+              const int kc = sid[e] == p.a_stream ? p.key_col_a : p.key_col_b;
+              if (kc >= 0) key[e] = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e);
+            }
+          }
+        }
       }
     }
-    if (!role) continue;
-    int bucket;
-    if (a.route_world > 0) {
-      if (key < 0) { set_err(a.err, ERR_KEY_RANGE); continue; }
-      bucket = (int)(key % a.route_world);
-    } else {
-      if (key < 0 || (key % p.key_stride) != p.key_offset) {
-        set_err(a.err, ERR_KEY_RANGE);
-        continue;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
+                            ((role_g >> e) & 1u) * ROLE_G;
+      if (!role) continue;
+      int bucket;
+      if (a.route_world > 0) {
+        if (key[e] < 0) { set_err(a.err, ERR_KEY_RANGE); continue; }
+        bucket = (int)(key[e] % a.route_world);
+      } else {
+        if (key[e] < 0 || (key[e] % p.key_stride) != p.key_offset) {
+          set_err(a.err, ERR_KEY_RANGE);
+          continue;
+        }
+        const int64_t kl = key[e] / p.key_stride;
+        if (kl >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
+        bucket = (int)(kl & (P - 1));
       }
-      const int64_t kl = key / p.key_stride;
-      if (kl >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
-      bucket = (int)(kl & (P - 1));
+      const uint32_t rank = atomicAdd(&hist[bucket], 1u);
+      // bits 0-10 rank in tile, 11-13 role, 14-25 bucket
+      packed[e] = ((uint32_t)bucket << 14) | (role << 11) | rank;
     }
-    const uint32_t rank = atomicAdd(&hist[bucket], 1u);
-    // bits 0-10 rank in tile, 11-13 role, 14-25 bucket
-    packed[e] = ((uint32_t)bucket << 14) | (role << 11) | rank;
   }
   __syncthreads();
   // exclusive scan of the P bucket counts (P <= 4096: 16 per thread)
   {
     const int per = (P + kPartThreads - 1) / kPartThreads;
-    uint32_t local[16];
     uint32_t sum = 0;
     for (int i = 0; i < per; ++i) {
       const int idx = tid * per + i;
-      local[i] = idx < P ? hist[idx] : 0u;
-      sum += local[i];
+      sum += idx < P ? hist[idx] : 0u;
     }
     uint32_t total;
     uint32_t off = block_excl_scan(sum, scratch, &total);
     for (int i = 0; i < per; ++i) {
       const int idx = tid * per + i;
-      if (idx < P) hist[idx] = off;
-      off += local[i];
+      if (idx < P) {
+        const uint32_t c = hist[idx];
+        hist[idx] = off;
+        off += c;
+      }
     }
     if (tid == 0) hist[P] = total;
   }
@@ -281,10 +415,11 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   uint16_t* toff = a.tile_off + tile * (int64_t)(P + 1);
   for (int i = tid; i <= P; i += kPartThreads) toff[i] = (uint16_t)hist[i];
 
+  const int64_t tbase = tile * (int64_t)a.tile_rows;
 #pragma unroll
-  for (int e = 0; e < kPartItems; ++e) {
+  for (int e = 0; e < E; ++e) {
     if (packed[e] == 0xffffffffu) continue;
-    const int64_t r = tbase + (int64_t)e * kPartThreads + tid;
+    const int64_t r = r0 + e;
     const uint32_t b = packed[e] >> 14, rank = packed[e] & 0x7ffu;
     const uint32_t role = (packed[e] >> 11) & 7u;
     const int64_t pos = tbase + hist[b] + rank;
@@ -315,8 +450,9 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   }
 }
 
-void launch_partition(const PartArgs& a, int64_t ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_partition, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s) {
+  if (vm) hipLaunchKernelGGL(k_partition<true>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+  else hipLaunchKernelGGL(k_partition<false>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
 }
 
 // ================================================================ k_walk ==
@@ -326,22 +462,37 @@ constexpr int kEntryRec = 64;   // working-list ids >= 64 name window records
 
 struct WalkLds {
   uint32_t seg[kWalkMaxTiles + 1];   // exclusive prefix of segment sizes
+  uint16_t lo[kWalkMaxTiles];        // segment start inside each tile
   uint32_t wrec[kWalkWindow];        // global record index per window slot
-  uint32_t wseq[kWalkWindow];        // chunk-relative sequence number
   uint16_t wkey[kWalkWindow];        // key within the bucket
   uint16_t sorted[kWalkWindow];      // window slots grouped by key, arrival order
   uint32_t kstart[kWalkMaxKeys + 1];
-  uint32_t kcur[kWalkMaxKeys];
-  uint16_t plist[kMaxPending * kWalkThreads]; // per-thread working list [i][tid]
-  uint64_t R[kMaxRegs * kWalkThreads];
+  union {
+    uint32_t kcur[kWalkMaxKeys];     // counting-sort cursors
+    uint32_t firstb[kWalkMaxKeys];   // closed form: first B (sorted pos) per key, or ~0
+  };
+  union {
+    uint32_t wseq[kWalkWindow];      // chunk-relative sequence number (sorting)
+    uint32_t v[kWalkWindow];         // closed form: output position scan
+  };
+  union {
+    struct {
+      uint32_t wts[kWalkWindow];     // closed form: event ts - ts_base per window slot
+      uint8_t wrole[kWalkWindow];
+      uint16_t nextb[kWalkWindow];   // next B in the key run (sorted pos), or kNone16
+      uint8_t cm[kWalkMaxKeys];      // carried partials completed by the first B
+      uint8_t cfirst[kWalkMaxKeys];  // first completed carried slot
+    } cf;
+    uint16_t plist[kMaxPending * kWalkThreads];   // general form: working lists [i][tid]
+  };
   uint32_t scratch[8];
   unsigned long long base;
   uint32_t t1;
 };
 
 struct MatchEnv {
-  const uint64_t* slot;    // pending entry captured words (slot+2) or nullptr
-  const uint64_t* arec;    // pending entry as an A record (rec+3) or nullptr
+  const uint64_t* slot;    // pending entry as a state slot (words: ts, seq, caps) or nullptr
+  const uint64_t* arec;    // pending entry as an A record, or nullptr
   const int32_t* cap_from_rec;
   const uint64_t* brec;    // completing B record
   __device__ uint64_t col(int c, int) const { return brec[3 + c]; }
@@ -351,9 +502,40 @@ struct MatchEnv {
   __device__ int64_t ts() const { return (int64_t)brec[2]; }
 };
 
-template <bool kEmit>
-__device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, int key_in_bucket, int bucket,
-                             unsigned long long out_pos) {
+__device__ __forceinline__ uint64_t eval_match(const VmArgs& vm, int prog, uint64_t* R,
+                                                         const MatchEnv& env, bool* isnull) {
+  return vm_eval(vm.code, vm.konst, prog, R, threadIdx.x, kWalkThreads, env, isnull);
+}
+
+template <bool kVm>
+__device__ __forceinline__ void emit_match(const WalkArgs& a, uint64_t* R, const MatchEnv& env,
+                                           unsigned long long pos) {
+  if ((int64_t)pos >= a.out.cap) {
+    set_err(a.err, ERR_OUT_CAP);
+    return;
+  }
+  for (int c = 0; c < a.out.ncols; ++c) {
+    const int src = a.out.src[c];
+    uint64_t v;
+    if (src >= SRC_CAP && src < SRC_REC) {
+      v = env.cap(src - SRC_CAP);
+    } else if (!kVm || (src >= SRC_REC && src < SRC_TS)) {
+      v = env.brec[3 + (src - SRC_REC)];
+    } else {
+      bool isnull = false;
+      v = eval_match(a.vm, a.out.prog[c], R, env, &isnull);
+      if (isnull) v = 0;
+    }
+    store_col(a.out.col[c], a.out.type[c], (int64_t)pos, v);
+  }
+  a.out.ts[pos] = (int64_t)env.brec[2];
+  a.out.seq[pos] = (int64_t)env.brec[1];
+}
+
+// General form: one lane walks one key's records in arrival order.
+template <bool kEmit, bool kVm>
+__device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key_in_bucket,
+                             int bucket, unsigned long long out_pos) {
   const PatternArgs& p = a.pat;
   const int tid = threadIdx.x;
   const int S = p.pending_slots;
@@ -366,7 +548,8 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, int key_in_bucket, i
 #define PL(i) L.plist[(i) * kWalkThreads + tid]
   for (int i = 0; i < n; ++i) PL(i) = (uint16_t)i;
   auto entry_ts = [&](int e) -> int64_t {
-    return e < kEntryRec ? (int64_t)sl[e * sw] : (int64_t)a.recs[(int64_t)L.wrec[e - kEntryRec] * rw + 2];
+    return e < kEntryRec ? (int64_t)sl[e * sw]
+                         : (int64_t)a.recs[(int64_t)L.wrec[e - kEntryRec] * rw + 2];
   };
   uint32_t matches = 0;
   const uint32_t r0 = L.kstart[key_in_bucket], r1 = L.kstart[key_in_bucket + 1];
@@ -389,28 +572,13 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, int key_in_bucket, i
         MatchEnv env{e < kEntryRec ? sl + (int64_t)e * sw : nullptr,
                      e < kEntryRec ? nullptr : a.recs + (int64_t)L.wrec[e - kEntryRec] * rw,
                      p.cap_from_rec, rec};
-        if (!g && p.g_walk_prog >= 0) {
+        if (kVm && !g && p.g_walk_prog >= 0) {
           bool isnull = false;
-          uint64_t v = vm_eval(a.vm.code, a.vm.konst, p.g_walk_prog, L.R, tid, kWalkThreads, env,
-                               &isnull);
+          uint64_t v = eval_match(a.vm, p.g_walk_prog, R, env, &isnull);
           g = !isnull && (v & 1u);
         }
         if (g) {
-          if (kEmit) {
-            const unsigned long long pos = out_pos + matches;
-            if ((int64_t)pos < a.out.cap) {
-              for (int c = 0; c < a.out.ncols; ++c) {
-                bool isnull = false;
-                uint64_t v = vm_eval(a.vm.code, a.vm.konst, a.out.prog[c], L.R, tid,
-                                     kWalkThreads, env, &isnull);
-                store_col(a.out.col[c], a.out.type[c], (int64_t)pos, isnull ? 0 : v);
-              }
-              a.out.ts[pos] = ts;
-              a.out.seq[pos] = (int64_t)rec[1];
-            } else {
-              set_err(a.err, ERR_OUT_CAP);
-            }
-          }
+          if (kEmit) emit_match<kVm>(a, R, env, out_pos + matches);
           ++matches;
           continue;   // completed partial is consumed (s2 is not `every`)
         }
@@ -459,38 +627,54 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, int key_in_bucket, i
   return matches;
 }
 
+// XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
+// §Workgroup dispatch), so consecutive buckets — which share tile-offset
+// cache lines — are given to blocks of one XCD.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_bucket(int bid, int nb) {
+  if (nb < 8 || (nb & 7)) return bid;
+  return (bid & 7) * (nb >> 3) + (bid >> 3);
+}
+
 }  // namespace
 
+// kVm = false: g is evaluated in the partition pass and every output attribute
+// is a direct copy (no interpreter in the walk).
+template <bool kVm>
 __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
   __shared__ WalkLds L;
+  __shared__ uint64_t R[kVm ? kMaxRegs * kWalkThreads : 1];   // VM registers, [reg][lane]
   const int tid = threadIdx.x;
-  const int bucket = blockIdx.x;
   const PatternArgs& p = a.pat;
   const int P = 1 << p.buckets_log2;
+  const int bucket = xcd_bucket(blockIdx.x, P);
   const int kpb = (int)((p.key_capacity + P - 1) >> p.buckets_log2);
   const int ntiles = a.ntiles;
+  const int rw = p.rec_words;
+  const int64_t ts_base = p.closed_form ? *a.ts_base : 0;
 
-  // segment sizes -> exclusive prefix over tiles
+  // segment starts and sizes -> exclusive prefix over tiles
   {
     const int per = (ntiles + kWalkThreads - 1) / kWalkThreads;   // <= 8
-    uint32_t local[8];
     uint32_t sum = 0;
     for (int i = 0; i < per; ++i) {
       const int t = tid * per + i;
-      uint32_t c = 0;
       if (t < ntiles) {
         const uint16_t* o = a.tile_off + (int64_t)t * (P + 1) + bucket;
-        c = (uint32_t)o[1] - (uint32_t)o[0];
+        const uint32_t lo = o[0], hi = o[1];
+        L.lo[t] = (uint16_t)lo;
+        L.seg[t] = hi - lo;   // temporarily the count
+        sum += hi - lo;
       }
-      local[i] = c;
-      sum += c;
     }
     uint32_t total;
     uint32_t off = block_excl_scan(sum, L.scratch, &total);
     for (int i = 0; i < per; ++i) {
       const int t = tid * per + i;
-      if (t < ntiles) L.seg[t] = off;
-      off += local[i];
+      if (t < ntiles) {
+        const uint32_t c = L.seg[t];
+        L.seg[t] = off;
+        off += c;
+      }
     }
     if (tid == 0) L.seg[ntiles] = total;
   }
@@ -515,44 +699,53 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     const uint32_t wbase = L.seg[t0];
     const uint32_t nrec = L.seg[t1] - wbase;
     if (nrec > kWalkWindow) set_err(a.err, ERR_WINDOW);
-    // gather the window: one thread per tile segment
-    for (int t = t0 + tid; t < t1; t += kWalkThreads) {
-      const uint16_t* o = a.tile_off + (int64_t)t * (P + 1) + bucket;
-      const uint32_t lo = o[0], hi = o[1];
-      const uint32_t pos = L.seg[t] - wbase;
-      for (uint32_t j = lo; j < hi; ++j) {
-        const uint32_t w = pos + (j - lo);
-        if (w >= kWalkWindow) break;
-        const uint32_t gi = (uint32_t)t * (uint32_t)a.tile_rows + j;
-        const uint64_t* rec = a.recs + (int64_t)gi * p.rec_words;
-        L.wrec[w] = gi;
-        L.wkey[w] = (uint16_t)((uint32_t)rec[0] >> p.buckets_log2);
-        L.wseq[w] = (uint32_t)((int64_t)rec[1] - a.seq_chunk0);
-      }
-    }
-    __syncthreads();
     const uint32_t nw = nrec < (uint32_t)kWalkWindow ? nrec : (uint32_t)kWalkWindow;
-    for (uint32_t w = tid; w < nw; w += kWalkThreads) atomicAdd(&L.kstart[L.wkey[w] + 1], 1u);
+    // gather the window: one lane per record, tile found by binary search
+    for (uint32_t w = tid; w < nw; w += kWalkThreads) {
+      int lo = t0, hi = t1 - 1;   // largest t with seg[t] - wbase <= w
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (L.seg[mid] - wbase <= w) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint32_t gi = (uint32_t)lo * (uint32_t)a.tile_rows + L.lo[lo] + (w - (L.seg[lo] - wbase));
+      const uint64_t* rec = a.recs + (int64_t)gi * rw;
+      const uint64_t h = rec[0];
+      L.wrec[w] = gi;
+      L.wkey[w] = (uint16_t)((uint32_t)h >> p.buckets_log2);
+      L.wseq[w] = (uint32_t)((int64_t)rec[1] - a.seq_chunk0);
+      if (p.closed_form) {
+        const int64_t dt = (int64_t)rec[2] - ts_base;
+        if (dt < 0 || dt > 0xffffffffll) set_err(a.err, ERR_ORDER);
+        L.cf.wts[w] = (uint32_t)dt;
+        L.cf.wrole[w] = (uint8_t)(h >> 32);
+      }
+      atomicAdd(&L.kstart[((uint32_t)h >> p.buckets_log2) + 1], 1u);
+    }
     __syncthreads();
     // exclusive scan of key counts (kstart[1..kpb] -> kstart[0..kpb])
     {
-      const int per = (kpb + kWalkThreads - 1) / kWalkThreads;   // <= 8
-      uint32_t local[8];
+      const int per = (kpb + kWalkThreads - 1) / kWalkThreads;   // <= 4
       uint32_t sum = 0;
       for (int i = 0; i < per; ++i) {
         const int k = tid * per + i;
-        local[i] = k < kpb ? L.kstart[k + 1] : 0u;
-        sum += local[i];
+        sum += k < kpb ? L.kstart[k + 1] : 0u;
       }
       uint32_t total;
       uint32_t off = block_excl_scan(sum, L.scratch, &total);
-      for (int i = 0; i < per; ++i) {
+      uint32_t cnt[4];
+      for (int i = 0; i < per && i < 4; ++i) {
+        const int k = tid * per + i;
+        cnt[i] = k < kpb ? L.kstart[k + 1] : 0u;
+      }
+      __syncthreads();
+      for (int i = 0; i < per && i < 4; ++i) {
         const int k = tid * per + i;
         if (k < kpb) {
           L.kstart[k] = off;
           L.kcur[k] = off;
+          off += cnt[i];
         }
-        off += local[i];
       }
       if (tid == 0) L.kstart[kpb] = total;
     }
@@ -582,25 +775,157 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       }
     }
     __syncthreads();
-    // pass 1: count matches per thread
-    uint32_t mine = 0;
-    for (int k = tid; k < kpb; k += kWalkThreads)
-      if (L.kstart[k + 1] > L.kstart[k]) mine += walk_key<false>(a, L, k, bucket, 0);
-    uint32_t total;
-    const uint32_t off = block_excl_scan(mine, L.scratch, &total);
-    if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
-    __syncthreads();
-    // pass 2: emit + commit state
-    unsigned long long pos = L.base + off;
-    for (int k = tid; k < kpb; k += kWalkThreads)
-      if (L.kstart[k + 1] > L.kstart[k]) pos += walk_key<true>(a, L, k, bucket, pos);
-    __syncthreads();
+
+    if (p.closed_form) {
+      // ---- closed form: A matches the next B of its key within W -----------
+      const int S = p.pending_slots, sw = p.slot_words;
+      for (int k = tid; k < kpb; k += kWalkThreads) {
+        const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
+        uint32_t nb = 0xffffffffu;
+        for (uint32_t q = r1; q-- > r0;) {
+          L.cf.nextb[q] = nb == 0xffffffffu ? kNone16 : (uint16_t)nb;
+          if (L.cf.wrole[L.sorted[q]] & ROLE_B) nb = q;
+        }
+        L.firstb[k] = nb;
+        uint8_t cm = 0, cf = 0;
+        if (r1 > r0 && nb != 0xffffffffu) {
+          const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
+          const int n0 = a.pcnt[kl];
+          const uint64_t* sl = a.slots + kl * (int64_t)S * sw;
+          const int64_t tb = (int64_t)L.cf.wts[L.sorted[nb]] + ts_base;
+          int first = n0;
+          for (int j = 0; j < n0; ++j) {
+            const int64_t d = tb - (int64_t)sl[(int64_t)j * sw];
+            if (p.within < 0 || (d < 0 ? -d : d) <= p.within) {
+              first = j;
+              break;
+            }
+          }
+          cm = (uint8_t)(n0 - first);
+          cf = (uint8_t)first;
+        }
+        L.cf.cm[k] = cm;
+        L.cf.cfirst[k] = cf;
+      }
+      __syncthreads();
+      // per-position match flag + carried count at run start -> scan input
+      constexpr int per = kWalkWindow / kWalkThreads;   // 8 contiguous positions per lane
+      uint32_t vals[per];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int i = 0; i < per; ++i) {
+        const uint32_t q = tid * per + i;
+        uint32_t v = 0;
+        if (q < nw) {
+          const int w = L.sorted[q];
+          const int k = L.wkey[w];
+          if ((L.cf.wrole[w] & ROLE_A) && L.cf.nextb[q] != kNone16) {
+            const int64_t d = (int64_t)L.cf.wts[L.sorted[L.cf.nextb[q]]] - (int64_t)L.cf.wts[w];
+            v = (p.within < 0 || (d < 0 ? -d : d) <= p.within) ? 1u : 0u;
+          }
+          if (q == L.kstart[k]) v += L.cf.cm[k];
+        }
+        vals[i] = v;
+        sum += v;
+      }
+      uint32_t total;
+      uint32_t off = block_excl_scan(sum, L.scratch, &total);
+#pragma unroll
+      for (int i = 0; i < per; ++i) {
+        L.v[tid * per + i] = off;
+        off += vals[i];
+      }
+      if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
+      __syncthreads();
+      const unsigned long long base = L.base;
+      // emit record matches (lane per position)
+      for (uint32_t q = tid; q < nw; q += kWalkThreads) {
+        const int w = L.sorted[q];
+        if (!(L.cf.wrole[w] & ROLE_A) || L.cf.nextb[q] == kNone16) continue;
+        const int wb = L.sorted[L.cf.nextb[q]];
+        const int64_t d = (int64_t)L.cf.wts[wb] - (int64_t)L.cf.wts[w];
+        if (p.within >= 0 && (d < 0 ? -d : d) > p.within) continue;
+        const int k = L.wkey[w];
+        const uint32_t extra = q == L.kstart[k] ? L.cf.cm[k] : 0u;
+        MatchEnv env{nullptr, a.recs + (int64_t)L.wrec[w] * rw, p.cap_from_rec,
+                     a.recs + (int64_t)L.wrec[wb] * rw};
+        emit_match<kVm>(a, R, env, base + L.v[q] + extra);
+      }
+      // emit carried matches and commit per-key state (lane per key)
+      for (int k = tid; k < kpb; k += kWalkThreads) {
+        const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
+        if (r1 == r0) continue;
+        const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
+        uint64_t* sl = a.slots + kl * (int64_t)S * sw;
+        const int n0 = a.pcnt[kl];
+        const uint32_t fb = L.firstb[k];
+        if (L.cf.cm[k]) {
+          const uint64_t* brec = a.recs + (int64_t)L.wrec[L.sorted[fb]] * rw;
+          for (int j = 0; j < L.cf.cm[k]; ++j) {
+            MatchEnv env{sl + (int64_t)(L.cf.cfirst[k] + j) * sw, nullptr, p.cap_from_rec, brec};
+            emit_match<kVm>(a, R, env, base + L.v[r0] + j);
+          }
+        }
+        // survivors: partials created after the last B (all of them if no B),
+        // pruned to those within W of the last start (event-time order).
+        uint32_t lastb = 0xffffffffu;
+        int64_t last_a_ts = INT64_MIN;
+        for (uint32_t q = r0; q < r1; ++q) {
+          const int w = L.sorted[q];
+          if (L.cf.wrole[w] & ROLE_B) lastb = q;
+          if (L.cf.wrole[w] & ROLE_A) last_a_ts = (int64_t)L.cf.wts[w] + ts_base;
+        }
+        const bool prune = p.within >= 0 && last_a_ts != INT64_MIN;
+        int n = 0;
+        if (lastb == 0xffffffffu) {   // carried partials survive, minus pruned ones
+          for (int j = 0; j < n0; ++j) {
+            const int64_t ets = (int64_t)sl[(int64_t)j * sw];
+            if (prune && last_a_ts - ets > p.within) continue;
+            if (n != j)
+              for (int x = 0; x < sw; ++x) sl[(int64_t)n * sw + x] = sl[(int64_t)j * sw + x];
+            ++n;
+          }
+        }
+        // (a record that is both B and A starts a partial after completing others)
+        for (uint32_t q = (lastb == 0xffffffffu ? r0 : lastb); q < r1; ++q) {
+          const int w = L.sorted[q];
+          if (!(L.cf.wrole[w] & ROLE_A)) continue;
+          if (prune && last_a_ts - ((int64_t)L.cf.wts[w] + ts_base) > p.within) continue;
+          if (n >= S) {
+            set_err(a.err, ERR_PENDING);
+            break;
+          }
+          const uint64_t* rec = a.recs + (int64_t)L.wrec[w] * rw;
+          uint64_t* dst = sl + (int64_t)n * sw;
+          dst[0] = rec[2];
+          dst[1] = rec[1];
+          for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[3 + p.cap_from_rec[c]];
+          ++n;
+        }
+        a.pcnt[kl] = (uint8_t)n;
+      }
+      __syncthreads();
+    } else {
+      // ---- general form: one NFA lane per key (count pass, emit pass) -------
+      uint32_t mine = 0;
+      for (int k = tid; k < kpb; k += kWalkThreads)
+        if (L.kstart[k + 1] > L.kstart[k]) mine += walk_key<false, kVm>(a, L, R, k, bucket, 0);
+      uint32_t total;
+      const uint32_t off = block_excl_scan(mine, L.scratch, &total);
+      if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
+      __syncthreads();
+      unsigned long long pos = L.base + off;
+      for (int k = tid; k < kpb; k += kWalkThreads)
+        if (L.kstart[k + 1] > L.kstart[k]) pos += walk_key<true, kVm>(a, L, R, k, bucket, pos);
+      __syncthreads();
+    }
     t0 = t1;
   }
 }
 
-void launch_walk(const WalkArgs& a, int nbuckets, hipStream_t s) {
-  hipLaunchKernelGGL(k_walk, dim3((unsigned)nbuckets), dim3(kWalkThreads), 0, s, a);
+void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s) {
+  if (vm) hipLaunchKernelGGL(k_walk<true>, dim3((unsigned)nbuckets), dim3(kWalkThreads), 0, s, a);
+  else hipLaunchKernelGGL(k_walk<false>, dim3((unsigned)nbuckets), dim3(kWalkThreads), 0, s, a);
 }
 
 // ============================================================ k_generate ==

@@ -65,6 +65,33 @@ struct Prog {
   bool valid() const { return off >= 0; }
 };
 
+// Interpreter-free predicate form: a flat AND (or OR) of up to kMaxTerms
+// atoms `(column [aop aconst]) cop cconst`, with Siddhi's numeric promotion
+// applied at compile time (atype = promote(column, aconst), ctype =
+// promote(atype, cconst); constants stored already converted).  Covers the
+// filters of every BASELINE config; anything else runs on the VM.
+constexpr int kMaxTerms = 4;
+struct Term {
+  int32_t col, coltype;
+  int32_t aop, atype;      // aop = 0: no arithmetic
+  uint64_t aconst;
+  int32_t cop, ctype;
+  uint64_t cconst;
+};
+struct TermList {
+  int32_t n = -1;          // -1: not expressible, use the VM program
+  int32_t any = 0;         // 0: all terms (AND), 1: any term (OR)
+  Term t[kMaxTerms];
+};
+
+// Output attribute sources that bypass the VM (plain attribute copies).
+enum : int32_t {
+  SRC_VM = -1,
+  SRC_CAP = 0,      // + i: captured word i of s1 (pattern) / column i (filter)
+  SRC_REC = 64,     // + i: record word i of the completing event (pattern)
+  SRC_TS = 128,     // event timestamp of the completing / current event
+};
+
 // Role bits carried in partition records (pattern path).
 enum : uint32_t {
   ROLE_A = 1u,        // event passes the start state's filter f

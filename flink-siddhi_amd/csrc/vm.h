@@ -297,3 +297,153 @@ __device__ __forceinline__ uint64_t vm_eval(const Ins* __restrict__ code,
 }
 
 }  // namespace cep
+
+namespace cep {
+
+// ---- global-address-space vector loads (avoid flat_load on generic pointers)
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gload4(const void* p) {
+  const v4u32 x = *(const __attribute__((address_space(1))) v4u32*)p;
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
+// ---- stage-wise evaluation of one predicate term over N rows ---------------
+// Each stage switches once on the (uniform) type / operator and then runs a
+// straight loop over the N values, instead of switching per element.
+template <int N>
+__device__ __forceinline__ void convert_run(uint64_t (&v)[N], int from, int to) {
+  if (from == to || to == T_LONG) return;
+  if (to == T_FLOAT) {
+    if (from == T_INT) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = from_f32((float)(int32_t)v[e]);
+    } else if (from == T_LONG) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = from_f32((float)(int64_t)v[e]);
+    }
+  } else if (to == T_DOUBLE) {
+    if (from == T_INT) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = from_f64((double)(int32_t)v[e]);
+    } else if (from == T_LONG) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = from_f64((double)(int64_t)v[e]);
+    } else if (from == T_FLOAT) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = from_f64((double)as_f32(v[e]));
+    }
+  }
+}
+
+#define CEP_RUN(expr)                     \
+  _Pragma("unroll") for (int e = 0; e < N; ++e) { expr; }
+
+template <int N>
+__device__ __forceinline__ void arith_run(uint64_t (&v)[N], int op, int t, uint64_t k,
+                                          uint32_t* nullm) {
+  switch (t) {
+    case T_INT: {
+      const int32_t y = (int32_t)k;
+      switch (op) {
+        case OP_ADD: CEP_RUN(v[e] = from_i32((int32_t)((uint32_t)v[e] + (uint32_t)y))) break;
+        case OP_SUB: CEP_RUN(v[e] = from_i32((int32_t)((uint32_t)v[e] - (uint32_t)y))) break;
+        case OP_MUL: CEP_RUN(v[e] = from_i32((int32_t)((uint32_t)v[e] * (uint32_t)y))) break;
+        case OP_DIV:
+          if (y == 0) { *nullm = ~0u; return; }
+          if (y == -1) { CEP_RUN(v[e] = from_i32((int32_t)(0u - (uint32_t)v[e]))) }
+          else { CEP_RUN(v[e] = from_i32((int32_t)v[e] / y)) }
+          break;
+        default:
+          if (y == 0) { *nullm = ~0u; return; }
+          if (y == -1) { CEP_RUN(v[e] = 0) }
+          else { CEP_RUN(v[e] = from_i32((int32_t)v[e] % y)) }
+          break;
+      }
+      return;
+    }
+    case T_LONG: {
+      const int64_t y = (int64_t)k;
+      switch (op) {
+        case OP_ADD: CEP_RUN(v[e] = v[e] + k) break;
+        case OP_SUB: CEP_RUN(v[e] = v[e] - k) break;
+        case OP_MUL: CEP_RUN(v[e] = v[e] * k) break;
+        case OP_DIV:
+          if (y == 0) { *nullm = ~0u; return; }
+          if (y == -1) { CEP_RUN(v[e] = 0ull - v[e]) }
+          else { CEP_RUN(v[e] = (uint64_t)((int64_t)v[e] / y)) }
+          break;
+        default:
+          if (y == 0) { *nullm = ~0u; return; }
+          if (y == -1) { CEP_RUN(v[e] = 0) }
+          else { CEP_RUN(v[e] = (uint64_t)((int64_t)v[e] % y)) }
+          break;
+      }
+      return;
+    }
+    case T_FLOAT: {
+      const float y = as_f32(k);
+      switch (op) {
+        case OP_ADD: CEP_RUN(v[e] = from_f32(as_f32(v[e]) + y)) break;
+        case OP_SUB: CEP_RUN(v[e] = from_f32(as_f32(v[e]) - y)) break;
+        case OP_MUL: CEP_RUN(v[e] = from_f32(as_f32(v[e]) * y)) break;
+        case OP_DIV: CEP_RUN(v[e] = from_f32(as_f32(v[e]) / y)) break;
+        default: CEP_RUN(v[e] = from_f32(fmodf(as_f32(v[e]), y))) break;
+      }
+      return;
+    }
+    default: {
+      const double y = as_f64(k);
+      switch (op) {
+        case OP_ADD: CEP_RUN(v[e] = from_f64(as_f64(v[e]) + y)) break;
+        case OP_SUB: CEP_RUN(v[e] = from_f64(as_f64(v[e]) - y)) break;
+        case OP_MUL: CEP_RUN(v[e] = from_f64(as_f64(v[e]) * y)) break;
+        case OP_DIV: CEP_RUN(v[e] = from_f64(as_f64(v[e]) / y)) break;
+        default: CEP_RUN(v[e] = from_f64(fmod(as_f64(v[e]), y))) break;
+      }
+      return;
+    }
+  }
+}
+
+template <int N, class T>
+__device__ __forceinline__ uint32_t cmp_run_t(const T (&x)[N], int op, T y) {
+  uint32_t b = 0;
+  switch (op) {
+    case OP_EQ: CEP_RUN(b |= (x[e] == y ? 1u : 0u) << e) break;
+    case OP_NE: CEP_RUN(b |= (x[e] != y ? 1u : 0u) << e) break;
+    case OP_LT: CEP_RUN(b |= (x[e] < y ? 1u : 0u) << e) break;
+    case OP_LE: CEP_RUN(b |= (x[e] <= y ? 1u : 0u) << e) break;
+    case OP_GT: CEP_RUN(b |= (x[e] > y ? 1u : 0u) << e) break;
+    default: CEP_RUN(b |= (x[e] >= y ? 1u : 0u) << e) break;
+  }
+  return b;
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t compare_run(const uint64_t (&v)[N], int op, int t, uint64_t k) {
+  switch (t) {
+    case T_LONG: {
+      int64_t x[N];
+      CEP_RUN(x[e] = (int64_t)v[e])
+      return cmp_run_t<N, int64_t>(x, op, (int64_t)k);
+    }
+    case T_FLOAT: {
+      float x[N];
+      CEP_RUN(x[e] = as_f32(v[e]))
+      return cmp_run_t<N, float>(x, op, as_f32(k));
+    }
+    case T_DOUBLE: {
+      double x[N];
+      CEP_RUN(x[e] = as_f64(v[e]))
+      return cmp_run_t<N, double>(x, op, as_f64(k));
+    }
+    default: {
+      int32_t x[N];
+      CEP_RUN(x[e] = (int32_t)v[e])
+      return cmp_run_t<N, int32_t>(x, op, (int32_t)k);
+    }
+  }
+}
+#undef CEP_RUN
+
+}  // namespace cep

@@ -1,3 +1,4 @@
+# GPU check: parity tests, smoke, bench (default size), rocprof kernel trace.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -5,5 +6,9 @@ timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 600 python bench.py --events 67108864 --steps 3 --warmup 1 --cpu-seconds 3 > gpurun_out/bench_small.log 2>&1
-exit $?
+timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || exit $?
+if [ -n "${PROF:-}" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || exit $?
+fi
+exit 0

@@ -223,9 +223,11 @@ def test_device_resident_batch_matches_host_batch():
 
 
 def test_pending_overflow_is_reported():
-    # 64 keys at 1 event/ms keep ~39 live partials per key in a 10 s window
+    # g never holds: every key keeps ~39 live partials inside the 10 s window
+    # (64 keys, 1 event/ms), more than 16 slots
     w = workload.generate(0, 30000, 64, rate=1)
-    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, pending_slots=16)
+    plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id == 1000")
+    rt = fs.SiddhiAppRuntime(plan, pending_slots=16)
     rt.add_callback("O")
     rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
     with pytest.raises(fs.CepCapacityError):
