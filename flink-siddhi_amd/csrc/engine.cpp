@@ -75,8 +75,8 @@ struct OutStream {
 struct PatternRT {
   int q = -1;
   PatternArgs pa{};
-  DevBuf pcnt, started, slots;
-  DevBuf recs, tile_off;
+  DevBuf kstate;             // [key][1 + S * slot_words] words
+  DevBuf recs, tile_off, chunk_base;
   int64_t chunk = 0;
   int64_t extra_bound = 0;   // pending partials that may still complete
   bool part_vm = true;       // partition pass needs the interpreter
@@ -255,8 +255,9 @@ int create_runtime(cep_app* a) {
     for (int i = 0; i < p.nrec_b; ++i) p.rec_b[i] = q.rec_cols_b[i];
     p.ncap = (int)q.cap_from_rec.size();
     for (int i = 0; i < p.ncap; ++i) p.cap_from_rec[i] = q.cap_from_rec[i];
-    p.rec_words = 3 + std::max(p.nrec_a, p.nrec_b);
+    p.rec_words = 2 + std::max(p.nrec_a, p.nrec_b);
     p.slot_words = 2 + p.ncap;
+    p.key_words = 1 + S * p.slot_words;
     p.pending_slots = S;
     const bool keyed = q.key_col_a >= 0;
     int64_t kcap = keyed ? a->opt.key_capacity : 1;
@@ -272,12 +273,10 @@ int create_runtime(cep_app* a) {
     if (!keyed) lg = 0;
     p.buckets_log2 = lg;
     const int64_t kc = kcap;
-    if (!dev_ensure(&rt.pcnt, (size_t)kc, a->stream, false) ||
-        !dev_ensure(&rt.started, (size_t)kc, a->stream, false) ||
-        !dev_ensure(&rt.slots, (size_t)kc * S * p.slot_words * 8, a->stream, false))
+    if (!dev_ensure(&rt.kstate, (size_t)kc * p.key_words * 8, a->stream, false) ||
+        !dev_ensure(&rt.chunk_base, 64, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (pattern state)");
-    hipMemset(rt.pcnt.p, 0, (size_t)kc);
-    hipMemset(rt.started.p, 0, (size_t)kc);
+    hipMemset(rt.kstate.p, 0, (size_t)kc * p.key_words * 8);
     int64_t chunk = a->opt.chunk_events;
     chunk = std::max<int64_t>(chunk, kPartThreads * kPartItems);
     chunk = std::min<int64_t>(chunk, (int64_t)kWalkMaxTiles * kPartThreads * kPartItems);
@@ -367,6 +366,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     pa.tile_rows = kPartThreads * kPartItems;
     pa.recs = (uint64_t*)rt.recs.p;
     pa.tile_off = (uint16_t*)rt.tile_off.p;
+    pa.chunk_base = (int64_t*)rt.chunk_base.p;
     pa.err = (unsigned int*)a->err.p;
     {
       LaunchTimer t(a, CEP_K_PARTITION);
@@ -379,11 +379,8 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     wa.tile_off = pa.tile_off;
     wa.ntiles = (int)ntiles;
     wa.tile_rows = pa.tile_rows;
-    wa.seq_chunk0 = rows.seq0 + rows.row0;
-    wa.ts_base = rows.ts + rows.row0;
-    wa.pcnt = (uint8_t*)rt.pcnt.p;
-    wa.started = (uint8_t*)rt.started.p;
-    wa.slots = (uint64_t*)rt.slots.p;
+    wa.chunk_base = (const int64_t*)rt.chunk_base.p;
+    wa.kstate = (uint64_t*)rt.kstate.p;
     wa.out = out_args(o, q);
     wa.err = pa.err;
     {
@@ -524,11 +521,10 @@ void cep_destroy(cep_app* a) {
     if (o.count) hipFree(o.count);
   }
   for (auto& p : a->pats) {
-    dev_free(&p.pcnt);
-    dev_free(&p.started);
-    dev_free(&p.slots);
+    dev_free(&p.kstate);
     dev_free(&p.recs);
     dev_free(&p.tile_off);
+    dev_free(&p.chunk_base);
   }
   for (auto& s : a->stage) dev_free(&s);
   dev_free(&a->code);
@@ -762,9 +758,9 @@ const char* cep_last_error(cep_app* a) { return a ? a->last_error.c_str() : "nul
 void cep_free(void* p) { std::free(p); }
 
 // Snapshot format (little endian):
-//   "CEPS" u32 version=1, u64 plan_hash, i64 events_in, u32 n_patterns,
+//   "CEPS" u32 version=2, u64 plan_hash, i64 events_in, u32 n_patterns,
 //   per pattern: i64 key_capacity, u32 S, u32 slot_words, u32 n_live,
-//                n_live x { u32 key, u8 cnt, u8 started, cnt*slot_words u64 }
+//                n_live x { u32 key, u64 header, (header & 0xff) * slot_words u64 }
 static uint64_t plan_hash(const CompiledApp& app) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](const void* p, size_t n) {
@@ -786,7 +782,7 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
   };
   const char magic[4] = {'C', 'E', 'P', 'S'};
   put(magic, 4);
-  uint32_t ver = 1;
+  uint32_t ver = 2;
   put(&ver, 4);
   uint64_t h = plan_hash(a->app);
   put(&h, 8);
@@ -795,25 +791,22 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
   put(&np, 4);
   for (auto& rt : a->pats) {
     const int64_t kc = rt.pa.key_capacity;
-    const uint32_t S = rt.pa.pending_slots, sw = rt.pa.slot_words;
-    std::vector<uint8_t> cnt(kc), st(kc);
-    hipMemcpy(cnt.data(), rt.pcnt.p, kc, hipMemcpyDeviceToHost);
-    hipMemcpy(st.data(), rt.started.p, kc, hipMemcpyDeviceToHost);
-    std::vector<uint64_t> slots((size_t)kc * S * sw);
-    hipMemcpy(slots.data(), rt.slots.p, slots.size() * 8, hipMemcpyDeviceToHost);
+    const uint32_t S = rt.pa.pending_slots, sw = rt.pa.slot_words, kw = rt.pa.key_words;
+    std::vector<uint64_t> st((size_t)kc * kw);
+    hipMemcpy(st.data(), rt.kstate.p, st.size() * 8, hipMemcpyDeviceToHost);
     uint32_t live = 0;
-    for (int64_t k = 0; k < kc; ++k) live += (cnt[k] || st[k]) ? 1 : 0;
+    for (int64_t k = 0; k < kc; ++k) live += st[(size_t)k * kw] ? 1 : 0;
     put(&kc, 8);
     put(&S, 4);
     put(&sw, 4);
     put(&live, 4);
     for (int64_t k = 0; k < kc; ++k) {
-      if (!cnt[k] && !st[k]) continue;
+      const uint64_t hdr = st[(size_t)k * kw];
+      if (!hdr) continue;
       uint32_t key = (uint32_t)k;
       put(&key, 4);
-      put(&cnt[k], 1);
-      put(&st[k], 1);
-      put(&slots[(size_t)k * S * sw], (size_t)cnt[k] * sw * 8);
+      put(&hdr, 8);
+      put(&st[(size_t)k * kw + 1], (size_t)(hdr & 0xff) * sw * 8);
     }
   }
   *buf = (uint8_t*)std::malloc(out.size());
@@ -837,7 +830,7 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   uint64_t h;
   int64_t ev;
   uint32_t np;
-  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver != 1 || !get(&h, 8) ||
+  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver != 2 || !get(&h, 8) ||
       !get(&ev, 8) || !get(&np, 4))
     return fail(a, CEP_E_STATE, "not a libcep snapshot");
   if (h != plan_hash(a->app) || np != a->pats.size())
@@ -851,21 +844,18 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     if (kc != rt.pa.key_capacity || S != (uint32_t)rt.pa.pending_slots ||
         sw != (uint32_t)rt.pa.slot_words)
       return fail(a, CEP_E_STATE, "snapshot geometry differs from this runtime");
-    std::vector<uint8_t> cnt(kc, 0), st(kc, 0);
-    std::vector<uint64_t> slots((size_t)kc * S * sw, 0);
+    const uint32_t kw = rt.pa.key_words;
+    std::vector<uint64_t> st((size_t)kc * kw, 0);
     for (uint32_t i = 0; i < live; ++i) {
       uint32_t key;
-      uint8_t c, s;
-      if (!get(&key, 4) || !get(&c, 1) || !get(&s, 1) || key >= kc || c > S)
+      uint64_t hdr;
+      if (!get(&key, 4) || !get(&hdr, 8) || key >= kc || (hdr & 0xff) > S)
         return fail(a, CEP_E_STATE, "corrupt snapshot");
-      cnt[key] = c;
-      st[key] = s;
-      if (!get(&slots[(size_t)key * S * sw], (size_t)c * sw * 8))
+      st[(size_t)key * kw] = hdr;
+      if (!get(&st[(size_t)key * kw + 1], (size_t)(hdr & 0xff) * sw * 8))
         return fail(a, CEP_E_STATE, "truncated snapshot");
     }
-    hipMemcpy(rt.pcnt.p, cnt.data(), kc, hipMemcpyHostToDevice);
-    hipMemcpy(rt.started.p, st.data(), kc, hipMemcpyHostToDevice);
-    hipMemcpy(rt.slots.p, slots.data(), slots.size() * 8, hipMemcpyHostToDevice);
+    hipMemcpy(rt.kstate.p, st.data(), st.size() * 8, hipMemcpyHostToDevice);
   }
   a->events_in = ev;
   return CEP_OK;

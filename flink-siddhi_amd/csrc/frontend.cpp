@@ -1239,11 +1239,30 @@ void compile_pattern(CompiledApp* app, QueryAst& q) {
   }
   for (auto& r : grefs)
     if (r.first == 0) out.g_in_walk = true;
+  if (q.partitioned) {
+    auto ia = q.partition.find(q.states[0].stream);
+    auto ib = q.partition.find(q.states[1].stream);
+    if (ia == q.partition.end() || ib == q.partition.end())
+      fail(CEP_E_PARSE, "pattern stream not covered by the enclosing partition");
+    out.key_col_a = key_column(A, ia->second);
+    out.key_col_b = key_column(B, ib->second);
+  }
+  // a select item that is just the partition key of s1 or s2 is emitted from
+  // the key itself (both states share it) and is not carried in records
+  auto is_key_ref = [&](const ExprP& e) {
+    return q.partitioned && e->k == Expr::ATTR && e->state >= 0 &&
+           e->col == (e->state == 0 ? out.key_col_a : out.key_col_b);
+  };
   // captured columns
   std::vector<int> cap_a, cap_b;
   if (out.g_in_walk)
     for (auto& r : grefs) index_of(r.first == 0 ? cap_a : cap_b, r.second, true);
-  for (auto& r : srefs) index_of(r.first == 0 ? cap_a : cap_b, r.second, true);
+  for (auto& it : q.select) {
+    if (is_key_ref(it.e)) continue;
+    std::vector<std::pair<int, int>> refs;
+    collect_refs(it.e, &refs);
+    for (auto& r : refs) index_of(r.first == 0 ? cap_a : cap_b, r.second, true);
+  }
   if ((int)cap_a.size() > kMaxCaps || (int)cap_b.size() > kMaxCaps)
     fail(CEP_E_UNSUPPORTED, "too many captured attributes");
   if (out.a_stream != out.b_stream) {
@@ -1288,21 +1307,18 @@ void compile_pattern(CompiledApp* app, QueryAst& q) {
     }
   }
   for (auto& it : q.select) {
-    CodeGen cg(app, walk);
     OutItem oi;
     oi.name = it.name;
     oi.type = it.e->t;
-    oi.prog = cg.compile(it.e);
-    oi.src = direct_source(app, oi.prog);   // SRC_CAP + i = s1 capture, SRC_REC + i = s2 word
+    if (is_key_ref(it.e)) {
+      oi.prog = Prog{};
+      oi.src = SRC_KEY;
+    } else {
+      CodeGen cg(app, walk);
+      oi.prog = cg.compile(it.e);
+      oi.src = direct_source(app, oi.prog);   // SRC_CAP + i = s1 capture, SRC_REC + i = s2 word
+    }
     out.select.push_back(oi);
-  }
-  if (q.partitioned) {
-    auto ia = q.partition.find(q.states[0].stream);
-    auto ib = q.partition.find(q.states[1].stream);
-    if (ia == q.partition.end() || ib == q.partition.end())
-      fail(CEP_E_PARSE, "pattern stream not covered by the enclosing partition");
-    out.key_col_a = key_column(A, ia->second);
-    out.key_col_b = key_column(B, ib->second);
   }
   add_output(app, q.out, out.select);
   app->queries.push_back(out);

@@ -84,8 +84,9 @@ struct PatternArgs {
   int32_t rec_a[kMaxCaps], rec_b[kMaxCaps];   // columns carried in records
   int32_t ncap;                                // captured words per pending slot
   int32_t cap_from_rec[kMaxCaps];
-  int32_t rec_words;       // 3 + max(nrec_a, nrec_b)
+  int32_t rec_words;       // 2 + max(nrec_a, nrec_b)
   int32_t slot_words;      // 2 + ncap
+  int32_t key_words;       // per-key state block: 1 header word + S * slot_words
   int32_t pending_slots;   // S
   int64_t key_capacity;    // dense keys per shard
   int32_t key_stride, key_offset;   // shard ownership (key % stride == offset)
@@ -97,8 +98,10 @@ struct PartArgs {
   RowsArgs rows;
   VmArgs vm;
   PatternArgs pat;
-  int32_t from_records;        // 1: input rows are records (multi-GPU receive)
-  const uint64_t* in_recs;     // records when from_records
+  int32_t from_records;        // 1: input rows are wide records (multi-GPU receive)
+  const uint64_t* in_recs;     // wide records [hdr, seq, ts, carried...] when from_records
+  int32_t in_rec_words;        // words per wide record
+  int64_t* chunk_base;         // out: {ts, seq} of the chunk's first row (read by k_walk)
   int32_t tile_rows;           // rows per tile (2048)
   uint64_t* recs;              // out: records, tile-major
   uint16_t* tile_off;          // out: [ntiles][P+1] exclusive offsets
@@ -113,12 +116,10 @@ struct WalkArgs {
   const uint16_t* tile_off;
   int32_t ntiles;
   int32_t tile_rows;
-  int64_t seq_chunk0;          // sequence number of the chunk's first row
-  const int64_t* ts_base;      // device: ts of the chunk's first row (closed form)
-  // per-key state (global, dense key index)
-  uint8_t* pcnt;
-  uint8_t* started;
-  uint64_t* slots;             // [key][S][slot_words]
+  const int64_t* chunk_base;   // device {ts, seq} of the chunk's first row
+  // per-key state (global, dense key index): block of key_words words,
+  // word 0 = pending count | started << 8, then S slots {ts, seq, caps...}
+  uint64_t* kstate;
   OutArgs out;
   unsigned int* err;
 };

@@ -274,20 +274,41 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) 
 }
 
 // =========================================================== k_partition ==
-// Record layout (8-byte words):
+// Record layout (8-byte words, chunk-relative):
 //   w0 = dense key (low 32) | role << 32 | input handle << 40
-//   w1 = arrival sequence number,  w2 = event timestamp,
-//   w3.. = carried columns (rec_a for A-stream rows, rec_b for B-stream rows)
+//   w1 = seq - chunk seq base (low 32) | ts - chunk ts base (high 32, signed)
+//   w2.. = carried columns (rec_a for A-stream rows, rec_b for B-stream rows)
+// Records of a tile are staged in LDS in bucket order and written out with
+// coalesced 16-byte stores (the tile's region is contiguous).
+constexpr int kStageBytes = 64 * 1024;
+
 template <bool kVm>
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
-  __shared__ uint64_t R[kMaxRegs * kPartThreads];
-  __shared__ uint32_t hist[4096 + 1];
+  __shared__ uint64_t R[kVm ? kMaxRegs * kPartThreads : 1];
   __shared__ uint32_t scratch[8];
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kStageBytes / 8];
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // P + 1 (dynamic)
   const int tid = threadIdx.x;
   const int64_t tile = blockIdx.x;
   const PatternArgs& p = a.pat;
   const int P = a.route_world > 0 ? a.route_world : (1 << p.buckets_log2);
+  const int rw = p.rec_words;
+  const bool staged = a.tile_rows * rw * 8 <= kStageBytes;
   for (int i = tid; i <= P; i += kPartThreads) hist[i] = 0;
+
+  // chunk bases: relative seq / ts in records
+  int64_t ts_base, seq_base;
+  if (a.from_records) {
+    ts_base = (int64_t)a.in_recs[a.rows.row0 * a.in_rec_words + 2];
+    seq_base = (int64_t)a.in_recs[a.rows.row0 * a.in_rec_words + 1];
+  } else {
+    ts_base = a.rows.ts[a.rows.row0];
+    seq_base = a.rows.seq0 + a.rows.row0;
+  }
+  if (tile == 0 && tid == 0 && a.chunk_base) {
+    a.chunk_base[0] = ts_base;
+    a.chunk_base[1] = seq_base;
+  }
   __syncthreads();
 
   constexpr int E = kPartItems;
@@ -297,15 +318,16 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
 #pragma unroll
   for (int e = 0; e < E; ++e) packed[e] = 0xffffffffu;
 
+  int64_t key[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) key[e] = 0;
   if (nvalid > 0) {
     uint32_t role_a = 0, role_b = 0, role_g = 0;
-    int64_t key[E];
     if (a.from_records) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        key[e] = 0;
         if (e < nvalid) {
-          const uint64_t h = a.in_recs[(r0 + e) * p.rec_words];
+          const uint64_t h = a.in_recs[(a.rows.row0 + r0 + e) * a.in_rec_words];
           const uint32_t role = (uint32_t)(h >> 32) & 0xffu;
           role_a |= ((role & ROLE_A) ? 1u : 0u) << e;
           role_b |= ((role & ROLE_B) ? 1u : 0u) << e;
@@ -373,86 +395,102 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
                             ((role_g >> e) & 1u) * ROLE_G;
       if (!role) continue;
       int bucket;
+      int64_t kfield;
       if (a.route_world > 0) {
         if (key[e] < 0) { set_err(a.err, ERR_KEY_RANGE); continue; }
         bucket = (int)(key[e] % a.route_world);
+        kfield = key[e];
       } else {
         if (key[e] < 0 || (key[e] % p.key_stride) != p.key_offset) {
           set_err(a.err, ERR_KEY_RANGE);
           continue;
         }
-        const int64_t kl = key[e] / p.key_stride;
-        if (kl >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
-        bucket = (int)(kl & (P - 1));
+        kfield = key[e] / p.key_stride;
+        if (kfield >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
+        bucket = (int)(kfield & (P - 1));
       }
+      key[e] = kfield;
       const uint32_t rank = atomicAdd(&hist[bucket], 1u);
       // bits 0-10 rank in tile, 11-13 role, 14-25 bucket
       packed[e] = ((uint32_t)bucket << 14) | (role << 11) | rank;
     }
   }
   __syncthreads();
-  // exclusive scan of the P bucket counts (P <= 4096: 16 per thread)
+  // exclusive scan of the P bucket counts (P <= 4096: 16 per thread); every
+  // thread of the block takes part (barriers inside)
   {
-    const int per = (P + kPartThreads - 1) / kPartThreads;
-    uint32_t sum = 0;
-    for (int i = 0; i < per; ++i) {
-      const int idx = tid * per + i;
-      sum += idx < P ? hist[idx] : 0u;
-    }
-    uint32_t total;
-    uint32_t off = block_excl_scan(sum, scratch, &total);
-    for (int i = 0; i < per; ++i) {
-      const int idx = tid * per + i;
-      if (idx < P) {
-        const uint32_t c = hist[idx];
-        hist[idx] = off;
-        off += c;
+      const int per = (P + kPartThreads - 1) / kPartThreads;
+      uint32_t sum = 0;
+      for (int i = 0; i < per; ++i) {
+        const int idx = tid * per + i;
+        sum += idx < P ? hist[idx] : 0u;
+      }
+      uint32_t total;
+      uint32_t off = block_excl_scan(sum, scratch, &total);
+      for (int i = 0; i < per; ++i) {
+        const int idx = tid * per + i;
+        if (idx < P) {
+          const uint32_t c = hist[idx];
+          hist[idx] = off;
+          off += c;
+        }
+      }
+      if (tid == 0) hist[P] = total;
+  }
+  __syncthreads();
+  {
+    // build the records (LDS stage when they fit, else straight to HBM)
+    const int64_t tbase = tile * (int64_t)a.tile_rows;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (packed[e] == 0xffffffffu) continue;
+      const uint32_t b = packed[e] >> 14, rank = packed[e] & 0x7ffu;
+      const uint32_t role = (packed[e] >> 11) & 7u;
+      const uint32_t slot = hist[b] + rank;
+      uint64_t* out = staged ? stage + (int64_t)slot * rw : a.recs + (tbase + slot) * rw;
+      const int64_t r = a.rows.row0 + r0 + e;
+      if (a.from_records) {
+        const uint64_t* in = a.in_recs + r * a.in_rec_words;
+        out[0] = (in[0] & ~0xffffffffull) | (uint64_t)(uint32_t)key[e];
+        out[1] = (uint64_t)(uint32_t)((int64_t)in[1] - seq_base) |
+                 ((uint64_t)(uint32_t)(int32_t)((int64_t)in[2] - ts_base) << 32);
+        for (int w = 2; w < rw; ++w) out[w] = in[w + 1];
+        continue;
+      }
+      const int s = a.rows.stream ? (int)a.rows.stream[r] : a.rows.input;
+      const int64_t dts = a.rows.ts[r] - ts_base;
+      if (dts > 0x7fffffffll || dts < -0x7fffffffll) set_err(a.err, ERR_ORDER);
+      out[0] = (uint64_t)(uint32_t)key[e] | ((uint64_t)role << 32) | ((uint64_t)(uint32_t)s << 40);
+      out[1] = (uint64_t)(uint32_t)(r - a.rows.row0) | ((uint64_t)(uint32_t)(int32_t)dts << 32);
+      const int nrc = s == p.a_stream ? p.nrec_a : p.nrec_b;
+      for (int c = 0; c < nrc; ++c) {
+        const int col = s == p.a_stream ? p.rec_a[c] : p.rec_b[c];
+        out[2 + c] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], r);
       }
     }
-    if (tid == 0) hist[P] = total;
   }
   __syncthreads();
   uint16_t* toff = a.tile_off + tile * (int64_t)(P + 1);
   for (int i = tid; i <= P; i += kPartThreads) toff[i] = (uint16_t)hist[i];
-
-  const int64_t tbase = tile * (int64_t)a.tile_rows;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    if (packed[e] == 0xffffffffu) continue;
-    const int64_t r = r0 + e;
-    const uint32_t b = packed[e] >> 14, rank = packed[e] & 0x7ffu;
-    const uint32_t role = (packed[e] >> 11) & 7u;
-    const int64_t pos = tbase + hist[b] + rank;
-    uint64_t* out = a.recs + pos * p.rec_words;
-    if (a.from_records) {
-      const uint64_t* in = a.in_recs + r * p.rec_words;
-      for (int w = 0; w < p.rec_words; ++w) out[w] = in[w];
-      if (a.route_world <= 0) {
-        const int64_t kl = (int64_t)(uint32_t)in[0] / p.key_stride;
-        out[0] = (in[0] & ~0xffffffffull) | (uint64_t)(uint32_t)kl;
+  if (staged) {
+    // the tile's records are contiguous in HBM: 16-byte coalesced stores
+    const int64_t words = (int64_t)hist[P] * rw;
+    uint64_t* dst = a.recs + tile * (int64_t)a.tile_rows * rw;
+    for (int64_t w = 2 * tid; w < words; w += 2 * kPartThreads) {
+      if (w + 1 < words) {
+        *(uint4*)(dst + w) = *(const uint4*)(stage + w);
+      } else {
+        dst[w] = stage[w];
       }
-      continue;
-    }
-    const int64_t row = a.rows.row0 + r;
-    const int s = a.rows.stream ? (int)a.rows.stream[row] : a.rows.input;
-    const int kc = s == p.a_stream ? p.key_col_a : p.key_col_b;
-    const int64_t key = kc >= 0 ? (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row) : 0;
-    const uint64_t kfield = a.route_world > 0 ? (uint64_t)(uint32_t)key
-                                              : (uint64_t)(uint32_t)(key / p.key_stride);
-    out[0] = kfield | ((uint64_t)role << 32) | ((uint64_t)(uint32_t)s << 40);
-    out[1] = (uint64_t)(a.rows.seq0 + row);
-    out[2] = (uint64_t)a.rows.ts[row];
-    const int nrc = s == p.a_stream ? p.nrec_a : p.nrec_b;
-    for (int c = 0; c < nrc; ++c) {
-      const int col = s == p.a_stream ? p.rec_a[c] : p.rec_b[c];
-      out[3 + c] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], row);
     }
   }
 }
 
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s) {
-  if (vm) hipLaunchKernelGGL(k_partition<true>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
-  else hipLaunchKernelGGL(k_partition<false>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+  const int P = a.route_world > 0 ? a.route_world : (1 << a.pat.buckets_log2);
+  const size_t dyn = ((size_t)(P + 1) * 4 + 15) & ~(size_t)15;
+  if (vm) hipLaunchKernelGGL(k_partition<true>, dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
+  else hipLaunchKernelGGL(k_partition<false>, dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
 }
 
 // ================================================================ k_walk ==
@@ -477,7 +515,7 @@ struct WalkLds {
   };
   union {
     struct {
-      uint32_t wts[kWalkWindow];     // closed form: event ts - ts_base per window slot
+      int32_t wts[kWalkWindow];      // closed form: chunk-relative event ts per window slot
       uint8_t wrole[kWalkWindow];
       uint16_t nextb[kWalkWindow];   // next B in the key run (sorted pos), or kNone16
       uint8_t cm[kWalkMaxKeys];      // carried partials completed by the first B
@@ -490,25 +528,35 @@ struct WalkLds {
   uint32_t t1;
 };
 
+// Chunk-relative record fields.
+__device__ __forceinline__ int64_t rec_ts(const uint64_t* rec, int64_t ts_base) {
+  return ts_base + (int64_t)(int32_t)(rec[1] >> 32);
+}
+__device__ __forceinline__ int64_t rec_seq(const uint64_t* rec, int64_t seq_base) {
+  return seq_base + (int64_t)(uint32_t)rec[1];
+}
+
 struct MatchEnv {
   const uint64_t* slot;    // pending entry as a state slot (words: ts, seq, caps) or nullptr
   const uint64_t* arec;    // pending entry as an A record, or nullptr
   const int32_t* cap_from_rec;
   const uint64_t* brec;    // completing B record
-  __device__ uint64_t col(int c, int) const { return brec[3 + c]; }
-  __device__ uint64_t cap(int i) const { return slot ? slot[2 + i] : arec[3 + cap_from_rec[i]]; }
+  int64_t ts_base;
+  __device__ uint64_t col(int c, int) const { return brec[2 + c]; }
+  __device__ uint64_t cap(int i) const { return slot ? slot[2 + i] : arec[2 + cap_from_rec[i]]; }
   __device__ uint64_t outv(int, bool* n) const { *n = true; return 0; }
   __device__ uint64_t agg(int, bool* n) const { *n = true; return 0; }
-  __device__ int64_t ts() const { return (int64_t)brec[2]; }
+  __device__ int64_t ts() const { return rec_ts(brec, ts_base); }
 };
 
 __device__ __forceinline__ uint64_t eval_match(const VmArgs& vm, int prog, uint64_t* R,
-                                                         const MatchEnv& env, bool* isnull) {
+                                               const MatchEnv& env, bool* isnull) {
   return vm_eval(vm.code, vm.konst, prog, R, threadIdx.x, kWalkThreads, env, isnull);
 }
 
 template <bool kVm>
 __device__ __forceinline__ void emit_match(const WalkArgs& a, uint64_t* R, const MatchEnv& env,
+                                           int64_t key, int64_t seq_base,
                                            unsigned long long pos) {
   if ((int64_t)pos >= a.out.cap) {
     set_err(a.err, ERR_OUT_CAP);
@@ -519,8 +567,10 @@ __device__ __forceinline__ void emit_match(const WalkArgs& a, uint64_t* R, const
     uint64_t v;
     if (src >= SRC_CAP && src < SRC_REC) {
       v = env.cap(src - SRC_CAP);
+    } else if (src == SRC_KEY) {
+      v = (uint64_t)key;
     } else if (!kVm || (src >= SRC_REC && src < SRC_TS)) {
-      v = env.brec[3 + (src - SRC_REC)];
+      v = env.brec[2 + (src - SRC_REC)];
     } else {
       bool isnull = false;
       v = eval_match(a.vm, a.out.prog[c], R, env, &isnull);
@@ -528,28 +578,36 @@ __device__ __forceinline__ void emit_match(const WalkArgs& a, uint64_t* R, const
     }
     store_col(a.out.col[c], a.out.type[c], (int64_t)pos, v);
   }
-  a.out.ts[pos] = (int64_t)env.brec[2];
-  a.out.seq[pos] = (int64_t)env.brec[1];
+  a.out.ts[pos] = env.ts();
+  a.out.seq[pos] = rec_seq(env.brec, seq_base);
+}
+
+// Original key value of dense key kl (shard ownership: key = kl*stride + offset).
+__device__ __forceinline__ int64_t key_value(const PatternArgs& p, int64_t kl) {
+  return kl * p.key_stride + p.key_offset;
 }
 
 // General form: one lane walks one key's records in arrival order.
 template <bool kEmit, bool kVm>
 __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key_in_bucket,
-                             int bucket, unsigned long long out_pos) {
+                             int bucket, int64_t ts_base, int64_t seq_base,
+                             unsigned long long out_pos) {
   const PatternArgs& p = a.pat;
   const int tid = threadIdx.x;
   const int S = p.pending_slots;
   const int sw = p.slot_words;
   const int rw = p.rec_words;
   const int64_t kl = ((int64_t)key_in_bucket << p.buckets_log2) | bucket;
-  uint64_t* sl = a.slots + kl * (int64_t)S * sw;
-  int n = a.pcnt[kl];
-  bool started = p.every ? false : (a.started[kl] != 0);
+  uint64_t* blk = a.kstate + kl * (int64_t)p.key_words;
+  uint64_t* sl = blk + 1;
+  const uint64_t hdr = blk[0];
+  int n = (int)(hdr & 0xffu);
+  bool started = p.every ? false : ((hdr >> 8) & 1u) != 0;
 #define PL(i) L.plist[(i) * kWalkThreads + tid]
   for (int i = 0; i < n; ++i) PL(i) = (uint16_t)i;
   auto entry_ts = [&](int e) -> int64_t {
     return e < kEntryRec ? (int64_t)sl[e * sw]
-                         : (int64_t)a.recs[(int64_t)L.wrec[e - kEntryRec] * rw + 2];
+                         : rec_ts(a.recs + (int64_t)L.wrec[e - kEntryRec] * rw, ts_base);
   };
   uint32_t matches = 0;
   const uint32_t r0 = L.kstart[key_in_bucket], r1 = L.kstart[key_in_bucket + 1];
@@ -558,7 +616,7 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
     const uint64_t* rec = a.recs + (int64_t)L.wrec[w] * rw;
     const uint64_t h = rec[0];
     const uint32_t role = (uint32_t)(h >> 32) & 0xffu;
-    const int64_t ts = (int64_t)rec[2];
+    const int64_t ts = rec_ts(rec, ts_base);
     if (role & ROLE_B) {
       int m = 0;
       for (int i = 0; i < n; ++i) {
@@ -571,14 +629,14 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
         bool g = (role & ROLE_G) != 0;
         MatchEnv env{e < kEntryRec ? sl + (int64_t)e * sw : nullptr,
                      e < kEntryRec ? nullptr : a.recs + (int64_t)L.wrec[e - kEntryRec] * rw,
-                     p.cap_from_rec, rec};
+                     p.cap_from_rec, rec, ts_base};
         if (kVm && !g && p.g_walk_prog >= 0) {
           bool isnull = false;
           uint64_t v = eval_match(a.vm, p.g_walk_prog, R, env, &isnull);
           g = !isnull && (v & 1u);
         }
         if (g) {
-          if (kEmit) emit_match<kVm>(a, R, env, out_pos + matches);
+          if (kEmit) emit_match<kVm>(a, R, env, key_value(p, kl), seq_base, out_pos + matches);
           ++matches;
           continue;   // completed partial is consumed (s2 is not `every`)
         }
@@ -615,13 +673,12 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
           for (int x = 0; x < sw; ++x) dst[x] = sl[(int64_t)e * sw + x];
       } else {
         const uint64_t* rec = a.recs + (int64_t)L.wrec[e - kEntryRec] * rw;
-        dst[0] = rec[2];
-        dst[1] = rec[1];
-        for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[3 + p.cap_from_rec[c]];
+        dst[0] = (uint64_t)rec_ts(rec, ts_base);
+        dst[1] = (uint64_t)rec_seq(rec, seq_base);
+        for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[2 + p.cap_from_rec[c]];
       }
     }
-    a.pcnt[kl] = (uint8_t)n;
-    if (!p.every) a.started[kl] = started ? 1 : 0;
+    blk[0] = (uint64_t)n | ((started ? 1ull : 0ull) << 8);
   }
 #undef PL
   return matches;
@@ -650,7 +707,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
   const int kpb = (int)((p.key_capacity + P - 1) >> p.buckets_log2);
   const int ntiles = a.ntiles;
   const int rw = p.rec_words;
-  const int64_t ts_base = p.closed_form ? *a.ts_base : 0;
+  const int64_t ts_base = a.chunk_base[0];
+  const int64_t seq_base = a.chunk_base[1];
 
   // segment starts and sizes -> exclusive prefix over tiles
   {
@@ -709,15 +767,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         else hi = mid - 1;
       }
       const uint32_t gi = (uint32_t)lo * (uint32_t)a.tile_rows + L.lo[lo] + (w - (L.seg[lo] - wbase));
-      const uint64_t* rec = a.recs + (int64_t)gi * rw;
-      const uint64_t h = rec[0];
+      const uint4 hv = gload4(a.recs + (int64_t)gi * rw);   // w0, w1 in one 16-byte load
+      const uint64_t h = ((uint64_t)hv.y << 32) | hv.x;
       L.wrec[w] = gi;
       L.wkey[w] = (uint16_t)((uint32_t)h >> p.buckets_log2);
-      L.wseq[w] = (uint32_t)((int64_t)rec[1] - a.seq_chunk0);
+      L.wseq[w] = hv.z;
       if (p.closed_form) {
-        const int64_t dt = (int64_t)rec[2] - ts_base;
-        if (dt < 0 || dt > 0xffffffffll) set_err(a.err, ERR_ORDER);
-        L.cf.wts[w] = (uint32_t)dt;
+        L.cf.wts[w] = (int32_t)hv.w;
         L.cf.wrole[w] = (uint8_t)(h >> 32);
       }
       atomicAdd(&L.kstart[((uint32_t)h >> p.buckets_log2) + 1], 1u);
@@ -726,19 +782,15 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     // exclusive scan of key counts (kstart[1..kpb] -> kstart[0..kpb])
     {
       const int per = (kpb + kWalkThreads - 1) / kWalkThreads;   // <= 4
+      uint32_t cnt[4];
       uint32_t sum = 0;
-      for (int i = 0; i < per; ++i) {
+      for (int i = 0; i < 4; ++i) {
         const int k = tid * per + i;
-        sum += k < kpb ? L.kstart[k + 1] : 0u;
+        cnt[i] = (i < per && k < kpb) ? L.kstart[k + 1] : 0u;
+        sum += cnt[i];
       }
       uint32_t total;
       uint32_t off = block_excl_scan(sum, L.scratch, &total);
-      uint32_t cnt[4];
-      for (int i = 0; i < per && i < 4; ++i) {
-        const int k = tid * per + i;
-        cnt[i] = k < kpb ? L.kstart[k + 1] : 0u;
-      }
-      __syncthreads();
       for (int i = 0; i < per && i < 4; ++i) {
         const int k = tid * per + i;
         if (k < kpb) {
@@ -790,12 +842,12 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         uint8_t cm = 0, cf = 0;
         if (r1 > r0 && nb != 0xffffffffu) {
           const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
-          const int n0 = a.pcnt[kl];
-          const uint64_t* sl = a.slots + kl * (int64_t)S * sw;
+          const uint64_t* blk = a.kstate + kl * (int64_t)p.key_words;
+          const int n0 = (int)(blk[0] & 0xffu);
           const int64_t tb = (int64_t)L.cf.wts[L.sorted[nb]] + ts_base;
           int first = n0;
           for (int j = 0; j < n0; ++j) {
-            const int64_t d = tb - (int64_t)sl[(int64_t)j * sw];
+            const int64_t d = tb - (int64_t)blk[1 + (int64_t)j * sw];
             if (p.within < 0 || (d < 0 ? -d : d) <= p.within) {
               first = j;
               break;
@@ -847,23 +899,26 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         if (p.within >= 0 && (d < 0 ? -d : d) > p.within) continue;
         const int k = L.wkey[w];
         const uint32_t extra = q == L.kstart[k] ? L.cf.cm[k] : 0u;
+        const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
         MatchEnv env{nullptr, a.recs + (int64_t)L.wrec[w] * rw, p.cap_from_rec,
-                     a.recs + (int64_t)L.wrec[wb] * rw};
-        emit_match<kVm>(a, R, env, base + L.v[q] + extra);
+                     a.recs + (int64_t)L.wrec[wb] * rw, ts_base};
+        emit_match<kVm>(a, R, env, key_value(p, kl), seq_base, base + L.v[q] + extra);
       }
       // emit carried matches and commit per-key state (lane per key)
       for (int k = tid; k < kpb; k += kWalkThreads) {
         const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
         if (r1 == r0) continue;
         const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
-        uint64_t* sl = a.slots + kl * (int64_t)S * sw;
-        const int n0 = a.pcnt[kl];
+        uint64_t* blk = a.kstate + kl * (int64_t)p.key_words;
+        uint64_t* sl = blk + 1;
+        const int n0 = (int)(blk[0] & 0xffu);
         const uint32_t fb = L.firstb[k];
         if (L.cf.cm[k]) {
           const uint64_t* brec = a.recs + (int64_t)L.wrec[L.sorted[fb]] * rw;
           for (int j = 0; j < L.cf.cm[k]; ++j) {
-            MatchEnv env{sl + (int64_t)(L.cf.cfirst[k] + j) * sw, nullptr, p.cap_from_rec, brec};
-            emit_match<kVm>(a, R, env, base + L.v[r0] + j);
+            MatchEnv env{sl + (int64_t)(L.cf.cfirst[k] + j) * sw, nullptr, p.cap_from_rec, brec,
+                         ts_base};
+            emit_match<kVm>(a, R, env, key_value(p, kl), seq_base, base + L.v[r0] + j);
           }
         }
         // survivors: partials created after the last B (all of them if no B),
@@ -890,33 +945,36 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         for (uint32_t q = (lastb == 0xffffffffu ? r0 : lastb); q < r1; ++q) {
           const int w = L.sorted[q];
           if (!(L.cf.wrole[w] & ROLE_A)) continue;
-          if (prune && last_a_ts - ((int64_t)L.cf.wts[w] + ts_base) > p.within) continue;
+          const int64_t ats = (int64_t)L.cf.wts[w] + ts_base;
+          if (prune && last_a_ts - ats > p.within) continue;
           if (n >= S) {
             set_err(a.err, ERR_PENDING);
             break;
           }
           const uint64_t* rec = a.recs + (int64_t)L.wrec[w] * rw;
           uint64_t* dst = sl + (int64_t)n * sw;
-          dst[0] = rec[2];
-          dst[1] = rec[1];
-          for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[3 + p.cap_from_rec[c]];
+          dst[0] = (uint64_t)ats;
+          dst[1] = (uint64_t)rec_seq(rec, seq_base);
+          for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[2 + p.cap_from_rec[c]];
           ++n;
         }
-        a.pcnt[kl] = (uint8_t)n;
+        blk[0] = (blk[0] & ~0xffull) | (uint64_t)n;
       }
       __syncthreads();
     } else {
       // ---- general form: one NFA lane per key (count pass, emit pass) -------
       uint32_t mine = 0;
       for (int k = tid; k < kpb; k += kWalkThreads)
-        if (L.kstart[k + 1] > L.kstart[k]) mine += walk_key<false, kVm>(a, L, R, k, bucket, 0);
+        if (L.kstart[k + 1] > L.kstart[k])
+          mine += walk_key<false, kVm>(a, L, R, k, bucket, ts_base, seq_base, 0);
       uint32_t total;
       const uint32_t off = block_excl_scan(mine, L.scratch, &total);
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
       __syncthreads();
       unsigned long long pos = L.base + off;
       for (int k = tid; k < kpb; k += kWalkThreads)
-        if (L.kstart[k + 1] > L.kstart[k]) pos += walk_key<true, kVm>(a, L, R, k, bucket, pos);
+        if (L.kstart[k + 1] > L.kstart[k])
+          pos += walk_key<true, kVm>(a, L, R, k, bucket, ts_base, seq_base, pos);
       __syncthreads();
     }
     t0 = t1;

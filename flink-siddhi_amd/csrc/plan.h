@@ -90,6 +90,7 @@ enum : int32_t {
   SRC_CAP = 0,      // + i: captured word i of s1 (pattern) / column i (filter)
   SRC_REC = 64,     // + i: record word i of the completing event (pattern)
   SRC_TS = 128,     // event timestamp of the completing / current event
+  SRC_KEY = 129,    // the partition key (pattern under `partition with`)
 };
 
 // Role bits carried in partition records (pattern path).
