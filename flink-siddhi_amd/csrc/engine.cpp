@@ -75,7 +75,8 @@ struct OutStream {
 struct PatternRT {
   int q = -1;
   PatternArgs pa{};
-  DevBuf kstate;             // [key][1 + S * slot_words] words
+  DevBuf khdr, kslot;        // per-key state, SoA over the bucket-major key index
+  int64_t kstride = 0;       // keys_per_bucket * buckets
   DevBuf recs, tile_off, chunk_base;
   int64_t chunk = 0;
   int64_t extra_bound = 0;   // pending partials that may still complete
@@ -102,6 +103,7 @@ struct cep_app {
   std::vector<OutStream> outs;
   std::vector<PatternRT> pats;
   DevBuf tile_state, ticket, err;
+  DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   std::vector<DevBuf> stage;   // host-batch staging columns (+ts, +stream)
   int64_t events_in = 0, matches_out = 0, batches = 0;
   int64_t last_ts = INT64_MIN;
@@ -245,7 +247,6 @@ int create_runtime(cep_app* a) {
     p.f_terms = q.f_terms;
     p.g_terms = q.g_terms;
     p.every = q.every ? 1 : 0;
-    p.closed_form = (q.every && !q.g_in_walk) ? 1 : 0;
     p.within = q.within;
     p.key_col_a = q.key_col_a;
     p.key_col_b = q.key_col_b;
@@ -259,6 +260,8 @@ int create_runtime(cep_app* a) {
     p.slot_words = 2 + p.ncap;
     p.key_words = 1 + S * p.slot_words;
     p.pending_slots = S;
+    // closed form keeps each record's carried words in LDS (kWalkCapLds)
+    p.closed_form = (q.every && !q.g_in_walk && p.rec_words <= 2 + kWalkCapLds) ? 1 : 0;
     const bool keyed = q.key_col_a >= 0;
     int64_t kcap = keyed ? a->opt.key_capacity : 1;
     p.key_capacity = kcap;
@@ -273,17 +276,20 @@ int create_runtime(cep_app* a) {
     if (!keyed) lg = 0;
     p.buckets_log2 = lg;
     const int64_t kc = kcap;
-    if (!dev_ensure(&rt.kstate, (size_t)kc * p.key_words * 8, a->stream, false) ||
+    const int64_t kpb = (kc + (1 << lg) - 1) >> lg;
+    rt.kstride = kpb << lg;
+    if (!dev_ensure(&rt.khdr, (size_t)rt.kstride * 4, a->stream, false) ||
+        !dev_ensure(&rt.kslot, (size_t)rt.kstride * S * p.slot_words * 8, a->stream, false) ||
         !dev_ensure(&rt.chunk_base, 64, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (pattern state)");
-    hipMemset(rt.kstate.p, 0, (size_t)kc * p.key_words * 8);
+    hipMemset(rt.khdr.p, 0, (size_t)rt.kstride * 4);
     int64_t chunk = a->opt.chunk_events;
     chunk = std::max<int64_t>(chunk, kPartThreads * kPartItems);
     chunk = std::min<int64_t>(chunk, (int64_t)kWalkMaxTiles * kPartThreads * kPartItems);
     chunk = (chunk / (kPartThreads * kPartItems)) * (kPartThreads * kPartItems);
     rt.chunk = chunk;
     const int64_t ntiles = chunk / (kPartThreads * kPartItems);
-    if (!dev_ensure(&rt.recs, (size_t)chunk * p.rec_words * 8, a->stream, false) ||
+    if (!dev_ensure(&rt.recs, (size_t)chunk * p.rec_words * 8 + 16, a->stream, false) ||
         !dev_ensure(&rt.tile_off, (size_t)ntiles * ((1 << lg) + 1) * 2, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
     rt.extra_bound = (int64_t)S * kc;
@@ -292,6 +298,8 @@ int create_runtime(cep_app* a) {
     for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
     a->pats.push_back(rt);
   }
+  if (std::getenv("CEP_STAMPS") && !dev_ensure(&a->stamps, (size_t)4096 * 16 * 8, a->stream, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory (stamps)");
   hipStreamSynchronize(a->stream);
   return CEP_OK;
 }
@@ -380,7 +388,13 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     wa.ntiles = (int)ntiles;
     wa.tile_rows = pa.tile_rows;
     wa.chunk_base = (const int64_t*)rt.chunk_base.p;
-    wa.kstate = (uint64_t*)rt.kstate.p;
+    if (a->stamps.p) {
+      // keep the last chunk's stamps (diagnostics only)
+      wa.stamps = (uint64_t*)a->stamps.p;
+    }
+    wa.khdr = (uint32_t*)rt.khdr.p;
+    wa.kslot = (uint64_t*)rt.kslot.p;
+    wa.kstride = rt.kstride;
     wa.out = out_args(o, q);
     wa.err = pa.err;
     {
@@ -512,6 +526,19 @@ cep_app* cep_create(const char* plan, const cep_options* opt, char* err, size_t 
 void cep_destroy(cep_app* a) {
   if (!a) return;
   if (a->stream) hipStreamSynchronize(a->stream);
+  if (a->stamps.p && !a->pats.empty()) {
+    // diagnostics: mean duration of each k_walk phase over the last launch's blocks
+    const int nb = 1 << a->pats[0].pa.buckets_log2;
+    std::vector<uint64_t> st((size_t)nb * 16);
+    hipMemcpy(st.data(), a->stamps.p, st.size() * 8, hipMemcpyDeviceToHost);
+    double sum[16] = {0};
+    for (int b = 0; b < nb; ++b)
+      for (int i = 1; i < 8; ++i)
+        if (st[b * 16 + i] && st[b * 16 + i - 1]) sum[i] += (double)(st[b * 16 + i] - st[b * 16 + i - 1]);
+    std::fprintf(stderr, "[cep stamps] k_walk phase ticks/block:");
+    for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);
+    std::fprintf(stderr, "\n");
+  }
   harvest_timers(a);
   for (auto e : a->event_pool) hipEventDestroy(e);
   for (auto& o : a->outs) {
@@ -521,7 +548,8 @@ void cep_destroy(cep_app* a) {
     if (o.count) hipFree(o.count);
   }
   for (auto& p : a->pats) {
-    dev_free(&p.kstate);
+    dev_free(&p.khdr);
+    dev_free(&p.kslot);
     dev_free(&p.recs);
     dev_free(&p.tile_off);
     dev_free(&p.chunk_base);
@@ -790,23 +818,28 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
   uint32_t np = (uint32_t)a->pats.size();
   put(&np, 4);
   for (auto& rt : a->pats) {
-    const int64_t kc = rt.pa.key_capacity;
-    const uint32_t S = rt.pa.pending_slots, sw = rt.pa.slot_words, kw = rt.pa.key_words;
-    std::vector<uint64_t> st((size_t)kc * kw);
-    hipMemcpy(st.data(), rt.kstate.p, st.size() * 8, hipMemcpyDeviceToHost);
+    const int64_t kc = rt.pa.key_capacity, ks = rt.kstride;
+    const uint32_t S = rt.pa.pending_slots, sw = rt.pa.slot_words;
+    const int lg = rt.pa.buckets_log2;
+    const int64_t kpb = ks >> lg;
+    std::vector<uint32_t> hdr(ks);
+    std::vector<uint64_t> slots((size_t)ks * S * sw);
+    hipMemcpy(hdr.data(), rt.khdr.p, hdr.size() * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(slots.data(), rt.kslot.p, slots.size() * 8, hipMemcpyDeviceToHost);
     uint32_t live = 0;
-    for (int64_t k = 0; k < kc; ++k) live += st[(size_t)k * kw] ? 1 : 0;
+    for (int64_t i = 0; i < ks; ++i) live += hdr[i] ? 1 : 0;
     put(&kc, 8);
     put(&S, 4);
     put(&sw, 4);
     put(&live, 4);
-    for (int64_t k = 0; k < kc; ++k) {
-      const uint64_t hdr = st[(size_t)k * kw];
-      if (!hdr) continue;
-      uint32_t key = (uint32_t)k;
+    for (int64_t i = 0; i < ks; ++i) {
+      if (!hdr[i]) continue;
+      const uint32_t key = (uint32_t)(((i % kpb) << lg) | (i / kpb));   // dense key
+      const uint64_t h64 = hdr[i];
       put(&key, 4);
-      put(&hdr, 8);
-      put(&st[(size_t)k * kw + 1], (size_t)(hdr & 0xff) * sw * 8);
+      put(&h64, 8);
+      for (uint32_t j = 0; j < (hdr[i] & 0xff); ++j)
+        for (uint32_t w = 0; w < sw; ++w) put(&slots[((size_t)j * sw + w) * ks + i], 8);
     }
   }
   *buf = (uint8_t*)std::malloc(out.size());
@@ -844,18 +877,25 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     if (kc != rt.pa.key_capacity || S != (uint32_t)rt.pa.pending_slots ||
         sw != (uint32_t)rt.pa.slot_words)
       return fail(a, CEP_E_STATE, "snapshot geometry differs from this runtime");
-    const uint32_t kw = rt.pa.key_words;
-    std::vector<uint64_t> st((size_t)kc * kw, 0);
+    const int64_t ks = rt.kstride;
+    const int lg = rt.pa.buckets_log2;
+    const int64_t kpb = ks >> lg;
+    std::vector<uint32_t> hdr(ks, 0);
+    std::vector<uint64_t> slots((size_t)ks * S * sw, 0);
     for (uint32_t i = 0; i < live; ++i) {
       uint32_t key;
-      uint64_t hdr;
-      if (!get(&key, 4) || !get(&hdr, 8) || key >= kc || (hdr & 0xff) > S)
+      uint64_t h64;
+      if (!get(&key, 4) || !get(&h64, 8) || key >= kc || (h64 & 0xff) > S)
         return fail(a, CEP_E_STATE, "corrupt snapshot");
-      st[(size_t)key * kw] = hdr;
-      if (!get(&st[(size_t)key * kw + 1], (size_t)(hdr & 0xff) * sw * 8))
-        return fail(a, CEP_E_STATE, "truncated snapshot");
+      const int64_t idx = (int64_t)(key & ((1u << lg) - 1)) * kpb + (key >> lg);
+      hdr[idx] = (uint32_t)h64;
+      for (uint32_t j = 0; j < (h64 & 0xff); ++j)
+        for (uint32_t w = 0; w < sw; ++w)
+          if (!get(&slots[((size_t)j * sw + w) * ks + idx], 8))
+            return fail(a, CEP_E_STATE, "truncated snapshot");
     }
-    hipMemcpy(rt.kstate.p, st.data(), st.size() * 8, hipMemcpyHostToDevice);
+    hipMemcpy(rt.khdr.p, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(rt.kslot.p, slots.data(), slots.size() * 8, hipMemcpyHostToDevice);
   }
   a->events_in = ev;
   return CEP_OK;

@@ -117,9 +117,14 @@ struct WalkArgs {
   int32_t ntiles;
   int32_t tile_rows;
   const int64_t* chunk_base;   // device {ts, seq} of the chunk's first row
-  // per-key state (global, dense key index): block of key_words words,
-  // word 0 = pending count | started << 8, then S slots {ts, seq, caps...}
-  uint64_t* kstate;
+  // per-key state, structure of arrays over the bucket-major key index
+  // idx = bucket * keys_per_bucket + key_in_bucket (a bucket's keys are contiguous):
+  //   khdr[idx]                    = pending count | started << 8
+  //   kslot[(j * slot_words + w) * kstride + idx] = word w of pending slot j
+  uint32_t* khdr;
+  uint64_t* kslot;
+  int64_t kstride;
+  uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per block 16 s_memtime stamps
   OutArgs out;
   unsigned int* err;
 };
@@ -137,10 +142,11 @@ constexpr int kFilterThreads = 256;
 constexpr int kFilterItems = 16;          // rows per thread per tile
 constexpr int kPartThreads = 256;
 constexpr int kPartItems = 8;             // tile = 2048 rows
-constexpr int kWalkThreads = 256;
-constexpr int kWalkWindow = 2048;         // records per LDS window
+constexpr int kWalkThreads = 512;
+constexpr int kWalkWindow = 1024;         // records per LDS window
 constexpr int kWalkMaxTiles = 2048;       // tiles per chunk
-constexpr int kWalkMaxKeys = 1024;        // keys per bucket (LDS histogram)
-constexpr int kMaxPending = 32;           // pending_slots upper bound
+constexpr int kWalkMaxKeys = 512;         // keys per bucket (LDS histogram)
+constexpr int kWalkCapLds = 2;            // carried record words kept in LDS (closed form)
+constexpr int kMaxPending = 16;           // pending_slots upper bound (walk LDS lists)
 
 }  // namespace cep

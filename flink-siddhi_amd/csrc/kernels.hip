@@ -37,10 +37,11 @@ __device__ __forceinline__ void set_err(unsigned int* err, unsigned int bit) {
   if (err) atomicOr(err, bit);
 }
 
-// Block-wide exclusive scan of one value per thread (blockDim = 256).
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch /*>=5*/,
+// Block-wide exclusive scan of one value per thread (blockDim <= 512).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch /*>=9*/,
                                                     uint32_t* total) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwaves = (int)(blockDim.x >> 6);
   uint32_t x = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -51,16 +52,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
   __syncthreads();
   if (tid == 0) {
     uint32_t s = 0;
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < nwaves; ++w) {
       uint32_t t = scratch[w];
       scratch[w] = s;
       s += t;
     }
-    scratch[4] = s;
+    scratch[8] = s;
   }
   __syncthreads();
   uint32_t r = scratch[wave] + x - v;
-  *total = scratch[4];
+  *total = scratch[8];
   __syncthreads();
   return r;
 }
@@ -175,7 +176,7 @@ __device__ __forceinline__ uint32_t eval_run(const TermList& tl, const VmArgs& v
 template <bool kVm>
 __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
   __shared__ uint64_t R[kMaxRegs * kFilterThreads];
-  __shared__ uint32_t scratch[8];
+  __shared__ uint32_t scratch[16];
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_prefix;
   const int tid = threadIdx.x;
@@ -280,12 +281,12 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) 
 //   w2.. = carried columns (rec_a for A-stream rows, rec_b for B-stream rows)
 // Records of a tile are staged in LDS in bucket order and written out with
 // coalesced 16-byte stores (the tile's region is contiguous).
-constexpr int kStageBytes = 64 * 1024;
+constexpr int kStageBytes = 16 * 1024;   // typical tiles keep ~10% of rows
 
 template <bool kVm>
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   __shared__ uint64_t R[kVm ? kMaxRegs * kPartThreads : 1];
-  __shared__ uint32_t scratch[8];
+  __shared__ uint32_t scratch[16];
   __shared__ __attribute__((aligned(16))) uint64_t stage[kStageBytes / 8];
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // P + 1 (dynamic)
   const int tid = threadIdx.x;
@@ -293,7 +294,6 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   const PatternArgs& p = a.pat;
   const int P = a.route_world > 0 ? a.route_world : (1 << p.buckets_log2);
   const int rw = p.rec_words;
-  const bool staged = a.tile_rows * rw * 8 <= kStageBytes;
   for (int i = tid; i <= P; i += kPartThreads) hist[i] = 0;
 
   // chunk bases: relative seq / ts in records
@@ -438,6 +438,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       if (tid == 0) hist[P] = total;
   }
   __syncthreads();
+  const bool staged = (int64_t)hist[P] * rw * 8 <= kStageBytes;   // uniform
   {
     // build the records (LDS stage when they fit, else straight to HBM)
     const int64_t tbase = tile * (int64_t)a.tile_rows;
@@ -497,6 +498,7 @@ void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s)
 namespace {
 
 constexpr int kEntryRec = 64;   // working-list ids >= 64 name window records
+constexpr int kWalkSlotStage = 2048;   // u64 words of staged per-key state (closed form)
 
 struct WalkLds {
   uint32_t seg[kWalkMaxTiles + 1];   // exclusive prefix of segment sizes
@@ -504,26 +506,25 @@ struct WalkLds {
   uint32_t wrec[kWalkWindow];        // global record index per window slot
   uint16_t wkey[kWalkWindow];        // key within the bucket
   uint16_t sorted[kWalkWindow];      // window slots grouped by key, arrival order
+  uint32_t wseq[kWalkWindow];        // chunk-relative sequence number
   uint32_t kstart[kWalkMaxKeys + 1];
-  union {
-    uint32_t kcur[kWalkMaxKeys];     // counting-sort cursors
-    uint32_t firstb[kWalkMaxKeys];   // closed form: first B (sorted pos) per key, or ~0
-  };
-  union {
-    uint32_t wseq[kWalkWindow];      // chunk-relative sequence number (sorting)
-    uint32_t v[kWalkWindow];         // closed form: output position scan
-  };
+  uint32_t khdr[kWalkMaxKeys];       // per-key state headers of this bucket (prefetched)
+  uint32_t kcur[kWalkMaxKeys];       // counting-sort cursors, then closed-form first B
   union {
     struct {
-      int32_t wts[kWalkWindow];      // closed form: chunk-relative event ts per window slot
-      uint8_t wrole[kWalkWindow];
+      int32_t wts[kWalkWindow];      // chunk-relative event ts per window slot
+      uint32_t v[kWalkWindow];       // output position scan
       uint16_t nextb[kWalkWindow];   // next B in the key run (sorted pos), or kNone16
+      uint8_t wrole[kWalkWindow];
       uint8_t cm[kWalkMaxKeys];      // carried partials completed by the first B
       uint8_t cfirst[kWalkMaxKeys];  // first completed carried slot
+      uint64_t wcap[kWalkWindow][kWalkCapLds];   // carried record words
+      uint64_t sstage[kWalkSlotStage];           // carried state slots of touched keys
+      uint16_t soff[kWalkMaxKeys];               // key's offset in sstage, or kNone16
     } cf;
     uint16_t plist[kMaxPending * kWalkThreads];   // general form: working lists [i][tid]
   };
-  uint32_t scratch[8];
+  uint32_t scratch[16];
   unsigned long long base;
   uint32_t t1;
 };
@@ -536,28 +537,49 @@ __device__ __forceinline__ int64_t rec_seq(const uint64_t* rec, int64_t seq_base
   return seq_base + (int64_t)(uint32_t)rec[1];
 }
 
+// Match environment of the general walk (records read from HBM).
 struct MatchEnv {
-  const uint64_t* slot;    // pending entry as a state slot (words: ts, seq, caps) or nullptr
+  const uint64_t* slot;    // pending entry as state slot word 0 (stride `sstride`) or nullptr
   const uint64_t* arec;    // pending entry as an A record, or nullptr
   const int32_t* cap_from_rec;
   const uint64_t* brec;    // completing B record
   int64_t ts_base;
+  int64_t sstride;         // words between consecutive words of one slot
   __device__ uint64_t col(int c, int) const { return brec[2 + c]; }
-  __device__ uint64_t cap(int i) const { return slot ? slot[2 + i] : arec[2 + cap_from_rec[i]]; }
+  __device__ uint64_t cap(int i) const {
+    return slot ? slot[(2 + i) * sstride] : arec[2 + cap_from_rec[i]];
+  }
   __device__ uint64_t outv(int, bool* n) const { *n = true; return 0; }
   __device__ uint64_t agg(int, bool* n) const { *n = true; return 0; }
   __device__ int64_t ts() const { return rec_ts(brec, ts_base); }
 };
 
-__device__ __forceinline__ uint64_t eval_match(const VmArgs& vm, int prog, uint64_t* R,
-                                               const MatchEnv& env, bool* isnull) {
+// Match environment of the closed form (record words already in LDS).
+struct CfEnv {
+  const uint64_t* acap;    // A words: LDS record words, or state slot word 0 (stride astride)
+  int64_t astride;         // 0: LDS record; else slot stride
+  const int32_t* cap_from_rec;
+  const uint64_t* bcap;    // completing B record words (LDS)
+  int64_t bts;
+  __device__ uint64_t col(int c, int) const { return bcap[c]; }
+  __device__ uint64_t cap(int i) const {
+    return astride ? acap[(2 + i) * astride] : acap[cap_from_rec[i]];
+  }
+  __device__ uint64_t outv(int, bool* n) const { *n = true; return 0; }
+  __device__ uint64_t agg(int, bool* n) const { *n = true; return 0; }
+  __device__ int64_t ts() const { return bts; }
+};
+
+template <class Env>
+__device__ __forceinline__ uint64_t eval_env(const VmArgs& vm, int prog, uint64_t* R,
+                                             const Env& env, bool* isnull) {
   return vm_eval(vm.code, vm.konst, prog, R, threadIdx.x, kWalkThreads, env, isnull);
 }
 
-template <bool kVm>
-__device__ __forceinline__ void emit_match(const WalkArgs& a, uint64_t* R, const MatchEnv& env,
-                                           int64_t key, int64_t seq_base,
-                                           unsigned long long pos) {
+// One output row.  `bword(c)` = completing event word c (src SRC_REC + c).
+template <bool kVm, class Env>
+__device__ __forceinline__ void emit_row(const WalkArgs& a, uint64_t* R, const Env& env,
+                                         int64_t key, int64_t seq, unsigned long long pos) {
   if ((int64_t)pos >= a.out.cap) {
     set_err(a.err, ERR_OUT_CAP);
     return;
@@ -570,16 +592,16 @@ __device__ __forceinline__ void emit_match(const WalkArgs& a, uint64_t* R, const
     } else if (src == SRC_KEY) {
       v = (uint64_t)key;
     } else if (!kVm || (src >= SRC_REC && src < SRC_TS)) {
-      v = env.brec[2 + (src - SRC_REC)];
+      v = env.col(src - SRC_REC, 0);
     } else {
       bool isnull = false;
-      v = eval_match(a.vm, a.out.prog[c], R, env, &isnull);
+      v = eval_env(a.vm, a.out.prog[c], R, env, &isnull);
       if (isnull) v = 0;
     }
     store_col(a.out.col[c], a.out.type[c], (int64_t)pos, v);
   }
   a.out.ts[pos] = env.ts();
-  a.out.seq[pos] = rec_seq(env.brec, seq_base);
+  a.out.seq[pos] = seq;
 }
 
 // Original key value of dense key kl (shard ownership: key = kl*stride + offset).
@@ -587,10 +609,17 @@ __device__ __forceinline__ int64_t key_value(const PatternArgs& p, int64_t kl) {
   return kl * p.key_stride + p.key_offset;
 }
 
+// Diagnostic phase stamps (null pointer = off).
+#define WALK_STAMP(i)                                                              \
+  do {                                                                              \
+    if (a.stamps && threadIdx.x == 0 && (i) < 16)                                   \
+      a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+
 // General form: one lane walks one key's records in arrival order.
 template <bool kEmit, bool kVm>
 __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key_in_bucket,
-                             int bucket, int64_t ts_base, int64_t seq_base,
+                             int bucket, int kpb, int64_t ts_base, int64_t seq_base,
                              unsigned long long out_pos) {
   const PatternArgs& p = a.pat;
   const int tid = threadIdx.x;
@@ -598,15 +627,17 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
   const int sw = p.slot_words;
   const int rw = p.rec_words;
   const int64_t kl = ((int64_t)key_in_bucket << p.buckets_log2) | bucket;
-  uint64_t* blk = a.kstate + kl * (int64_t)p.key_words;
-  uint64_t* sl = blk + 1;
-  const uint64_t hdr = blk[0];
+  const int64_t idx = (int64_t)bucket * kpb + key_in_bucket;
+  const int64_t ks = a.kstride;
+  uint64_t* sl = a.kslot + idx;                       // slot j word w: sl[(j * sw + w) * ks]
+  const uint32_t hdr = L.khdr[key_in_bucket];
   int n = (int)(hdr & 0xffu);
   bool started = p.every ? false : ((hdr >> 8) & 1u) != 0;
 #define PL(i) L.plist[(i) * kWalkThreads + tid]
+#define SW(j, w) sl[((int64_t)(j) * sw + (w)) * ks]
   for (int i = 0; i < n; ++i) PL(i) = (uint16_t)i;
   auto entry_ts = [&](int e) -> int64_t {
-    return e < kEntryRec ? (int64_t)sl[e * sw]
+    return e < kEntryRec ? (int64_t)SW(e, 0)
                          : rec_ts(a.recs + (int64_t)L.wrec[e - kEntryRec] * rw, ts_base);
   };
   uint32_t matches = 0;
@@ -627,16 +658,17 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
           if ((d < 0 ? -d : d) > p.within) continue;   // expired: dropped
         }
         bool g = (role & ROLE_G) != 0;
-        MatchEnv env{e < kEntryRec ? sl + (int64_t)e * sw : nullptr,
-                     e < kEntryRec ? nullptr : a.recs + (int64_t)L.wrec[e - kEntryRec] * rw,
-                     p.cap_from_rec, rec, ts_base};
+        const MatchEnv env{e < kEntryRec ? &SW(e, 0) : nullptr,
+                           e < kEntryRec ? nullptr : a.recs + (int64_t)L.wrec[e - kEntryRec] * rw,
+                           p.cap_from_rec, rec, ts_base, ks};
         if (kVm && !g && p.g_walk_prog >= 0) {
           bool isnull = false;
-          uint64_t v = eval_match(a.vm, p.g_walk_prog, R, env, &isnull);
+          uint64_t v = eval_env(a.vm, p.g_walk_prog, R, env, &isnull);
           g = !isnull && (v & 1u);
         }
         if (g) {
-          if (kEmit) emit_match<kVm>(a, R, env, key_value(p, kl), seq_base, out_pos + matches);
+          if (kEmit)
+            emit_row<kVm>(a, R, env, key_value(p, kl), rec_seq(rec, seq_base), out_pos + matches);
           ++matches;
           continue;   // completed partial is consumed (s2 is not `every`)
         }
@@ -667,19 +699,21 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
   if (kEmit) {
     for (int j = 0; j < n; ++j) {
       const int e = PL(j);
-      uint64_t* dst = sl + (int64_t)j * sw;
       if (e < kEntryRec) {
         if (e != j)
-          for (int x = 0; x < sw; ++x) dst[x] = sl[(int64_t)e * sw + x];
+          for (int x = 0; x < sw; ++x) SW(j, x) = SW(e, x);
       } else {
         const uint64_t* rec = a.recs + (int64_t)L.wrec[e - kEntryRec] * rw;
-        dst[0] = (uint64_t)rec_ts(rec, ts_base);
-        dst[1] = (uint64_t)rec_seq(rec, seq_base);
-        for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[2 + p.cap_from_rec[c]];
+        SW(j, 0) = (uint64_t)rec_ts(rec, ts_base);
+        SW(j, 1) = (uint64_t)rec_seq(rec, seq_base);
+        for (int c = 0; c < p.ncap; ++c) SW(j, 2 + c) = rec[2 + p.cap_from_rec[c]];
       }
     }
-    blk[0] = (uint64_t)n | ((started ? 1ull : 0ull) << 8);
+    const uint32_t nh = (uint32_t)n | ((started ? 1u : 0u) << 8);
+    L.khdr[key_in_bucket] = nh;   // next window of this bucket reads the LDS copy
+    a.khdr[idx] = nh;
   }
+#undef SW
 #undef PL
   return matches;
 }
@@ -707,41 +741,51 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
   const int kpb = (int)((p.key_capacity + P - 1) >> p.buckets_log2);
   const int ntiles = a.ntiles;
   const int rw = p.rec_words;
+  const int ncw = rw - 2;   // carried words per record
+  WALK_STAMP(0);
   const int64_t ts_base = a.chunk_base[0];
   const int64_t seq_base = a.chunk_base[1];
+  const int64_t ks = a.kstride;
+  // this bucket's per-key headers: kpb consecutive words (bucket-major index)
+  for (int k = tid; k < kpb; k += kWalkThreads) L.khdr[k] = a.khdr[(int64_t)bucket * kpb + k];
 
   // segment starts and sizes -> exclusive prefix over tiles
   {
-    const int per = (ntiles + kWalkThreads - 1) / kWalkThreads;   // <= 8
+    const int per = (ntiles + kWalkThreads - 1) / kWalkThreads;   // <= 4
+    uint32_t cnt[4];
     uint32_t sum = 0;
-    for (int i = 0; i < per; ++i) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
       const int t = tid * per + i;
-      if (t < ntiles) {
+      cnt[i] = 0;
+      if (i < per && t < ntiles) {
         const uint16_t* o = a.tile_off + (int64_t)t * (P + 1) + bucket;
         const uint32_t lo = o[0], hi = o[1];
         L.lo[t] = (uint16_t)lo;
-        L.seg[t] = hi - lo;   // temporarily the count
-        sum += hi - lo;
+        cnt[i] = hi - lo;
       }
+      sum += cnt[i];
     }
     uint32_t total;
     uint32_t off = block_excl_scan(sum, L.scratch, &total);
-    for (int i = 0; i < per; ++i) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
       const int t = tid * per + i;
-      if (t < ntiles) {
-        const uint32_t c = L.seg[t];
+      if (i < per && t < ntiles) {
         L.seg[t] = off;
-        off += c;
+        off += cnt[i];
       }
     }
     if (tid == 0) L.seg[ntiles] = total;
   }
   __syncthreads();
+  WALK_STAMP(1);
 
   int t0 = 0;
   while (t0 < ntiles) {
     if (tid == 0) {
-      // largest t1 with seg[t1] - seg[t0] <= window (a single tile always fits)
+      // largest t1 with seg[t1] - seg[t0] <= window (a single tile's segment is
+      // at most tile_rows = 2048 > window: such a tile is split below)
       int lo = t0 + 1, hi = ntiles;
       const uint32_t lim = L.seg[t0] + kWalkWindow;
       while (lo < hi) {
@@ -756,48 +800,45 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     const int t1 = (int)L.t1;
     const uint32_t wbase = L.seg[t0];
     const uint32_t nrec = L.seg[t1] - wbase;
-    if (nrec > kWalkWindow) set_err(a.err, ERR_WINDOW);
+    if (nrec > kWalkWindow) {   // one tile holds more than a window of this bucket
+      set_err(a.err, ERR_WINDOW);
+    }
     const uint32_t nw = nrec < (uint32_t)kWalkWindow ? nrec : (uint32_t)kWalkWindow;
-    // gather the window: one lane per record, tile found by binary search
+    // gather the window: record indices per tile segment (LDS only), then one
+    // independent 16-byte header load (+ carried words) per record
+    for (int t = t0 + tid; t < t1; t += kWalkThreads) {
+      const uint32_t pos = L.seg[t] - wbase, cnt = L.seg[t + 1] - L.seg[t];
+      const uint32_t g0 = (uint32_t)t * (uint32_t)a.tile_rows + L.lo[t];
+      for (uint32_t j = 0; j < cnt && pos + j < (uint32_t)kWalkWindow; ++j) L.wrec[pos + j] = g0 + j;
+    }
+    __syncthreads();
     for (uint32_t w = tid; w < nw; w += kWalkThreads) {
-      int lo = t0, hi = t1 - 1;   // largest t with seg[t] - wbase <= w
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (L.seg[mid] - wbase <= w) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint32_t gi = (uint32_t)lo * (uint32_t)a.tile_rows + L.lo[lo] + (w - (L.seg[lo] - wbase));
-      const uint4 hv = gload4(a.recs + (int64_t)gi * rw);   // w0, w1 in one 16-byte load
+      const uint64_t* rec = a.recs + (int64_t)L.wrec[w] * rw;
+      const uint4 hv = gload4(rec);   // w0, w1 in one 16-byte load
+      uint4 cv = make_uint4(0, 0, 0, 0);
+      if (p.closed_form && ncw > 0) cv = gload4(rec + 2);
       const uint64_t h = ((uint64_t)hv.y << 32) | hv.x;
-      L.wrec[w] = gi;
       L.wkey[w] = (uint16_t)((uint32_t)h >> p.buckets_log2);
       L.wseq[w] = hv.z;
       if (p.closed_form) {
         L.cf.wts[w] = (int32_t)hv.w;
         L.cf.wrole[w] = (uint8_t)(h >> 32);
+        L.cf.wcap[w][0] = ((uint64_t)cv.y << 32) | cv.x;
+        L.cf.wcap[w][1] = ((uint64_t)cv.w << 32) | cv.z;
       }
       atomicAdd(&L.kstart[((uint32_t)h >> p.buckets_log2) + 1], 1u);
     }
     __syncthreads();
+    WALK_STAMP(2);
     // exclusive scan of key counts (kstart[1..kpb] -> kstart[0..kpb])
     {
-      const int per = (kpb + kWalkThreads - 1) / kWalkThreads;   // <= 4
-      uint32_t cnt[4];
-      uint32_t sum = 0;
-      for (int i = 0; i < 4; ++i) {
-        const int k = tid * per + i;
-        cnt[i] = (i < per && k < kpb) ? L.kstart[k + 1] : 0u;
-        sum += cnt[i];
-      }
+      const int per = (kpb + kWalkThreads - 1) / kWalkThreads;   // <= 1
+      const uint32_t c = (tid < kpb) ? L.kstart[tid + 1] : 0u;
       uint32_t total;
-      uint32_t off = block_excl_scan(sum, L.scratch, &total);
-      for (int i = 0; i < per && i < 4; ++i) {
-        const int k = tid * per + i;
-        if (k < kpb) {
-          L.kstart[k] = off;
-          L.kcur[k] = off;
-          off += cnt[i];
-        }
+      const uint32_t off = block_excl_scan(per ? c : 0u, L.scratch, &total);
+      if (tid < kpb) {
+        L.kstart[tid] = off;
+        L.kcur[tid] = off;
       }
       if (tid == 0) L.kstart[kpb] = total;
     }
@@ -827,10 +868,36 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       }
     }
     __syncthreads();
+    WALK_STAMP(3);
 
     if (p.closed_form) {
       // ---- closed form: A matches the next B of its key within W -----------
       const int S = p.pending_slots, sw = p.slot_words;
+      // stage the carried state slots of every touched key in LDS: all global
+      // loads of the window are issued here, back to back, so the emission and
+      // commit below are LDS reads + HBM stores only
+      {
+        uint32_t need = 0;
+        if (tid < kpb && L.kstart[tid + 1] > L.kstart[tid]) need = (L.khdr[tid] & 0xffu) * (uint32_t)sw;
+        uint32_t total;
+        const uint32_t off = block_excl_scan(need, L.scratch, &total);
+        if (tid < kpb) {
+          const bool fits = off + need <= (uint32_t)kWalkSlotStage;
+          L.cf.soff[tid] = fits ? (uint16_t)off : kNone16;
+          if (fits && need) {
+            const uint64_t* sl = a.kslot + (int64_t)bucket * kpb + tid;
+            uint64_t* st = L.cf.sstage + off;
+            uint32_t i = 0;
+            for (; i + 4 <= need; i += 4) {
+              const uint64_t x0 = sl[(int64_t)i * ks], x1 = sl[(int64_t)(i + 1) * ks];
+              const uint64_t x2 = sl[(int64_t)(i + 2) * ks], x3 = sl[(int64_t)(i + 3) * ks];
+              st[i] = x0; st[i + 1] = x1; st[i + 2] = x2; st[i + 3] = x3;
+            }
+            for (; i < need; ++i) st[i] = sl[(int64_t)i * ks];
+          }
+        }
+      }
+      __syncthreads();
       for (int k = tid; k < kpb; k += kWalkThreads) {
         const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
         uint32_t nb = 0xffffffffu;
@@ -838,16 +905,18 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
           L.cf.nextb[q] = nb == 0xffffffffu ? kNone16 : (uint16_t)nb;
           if (L.cf.wrole[L.sorted[q]] & ROLE_B) nb = q;
         }
-        L.firstb[k] = nb;
+        L.kcur[k] = nb;   // first B of the run
         uint8_t cm = 0, cf = 0;
-        if (r1 > r0 && nb != 0xffffffffu) {
-          const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
-          const uint64_t* blk = a.kstate + kl * (int64_t)p.key_words;
-          const int n0 = (int)(blk[0] & 0xffu);
+        const int n0 = (int)(L.khdr[k] & 0xffu);
+        if (r1 > r0 && nb != 0xffffffffu && n0) {
+          const uint16_t so = L.cf.soff[k];
+          const uint64_t* sl = a.kslot + (int64_t)bucket * kpb + k;
           const int64_t tb = (int64_t)L.cf.wts[L.sorted[nb]] + ts_base;
           int first = n0;
           for (int j = 0; j < n0; ++j) {
-            const int64_t d = tb - (int64_t)blk[1 + (int64_t)j * sw];
+            const int64_t ets = so != kNone16 ? (int64_t)L.cf.sstage[so + j * sw]
+                                              : (int64_t)sl[(int64_t)j * sw * ks];
+            const int64_t d = tb - ets;
             if (p.within < 0 || (d < 0 ? -d : d) <= p.within) {
               first = j;
               break;
@@ -860,8 +929,9 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         L.cf.cfirst[k] = cf;
       }
       __syncthreads();
+      WALK_STAMP(4);
       // per-position match flag + carried count at run start -> scan input
-      constexpr int per = kWalkWindow / kWalkThreads;   // 8 contiguous positions per lane
+      constexpr int per = kWalkWindow / kWalkThreads;   // 2 contiguous positions per lane
       uint32_t vals[per];
       uint32_t sum = 0;
 #pragma unroll
@@ -884,13 +954,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       uint32_t off = block_excl_scan(sum, L.scratch, &total);
 #pragma unroll
       for (int i = 0; i < per; ++i) {
-        L.v[tid * per + i] = off;
+        L.cf.v[tid * per + i] = off;
         off += vals[i];
       }
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
       __syncthreads();
+      WALK_STAMP(5);
       const unsigned long long base = L.base;
-      // emit record matches (lane per position)
+      // emit record matches (lane per position; record words in LDS: stores only)
       for (uint32_t q = tid; q < nw; q += kWalkThreads) {
         const int w = L.sorted[q];
         if (!(L.cf.wrole[w] & ROLE_A) || L.cf.nextb[q] == kNone16) continue;
@@ -900,25 +971,30 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         const int k = L.wkey[w];
         const uint32_t extra = q == L.kstart[k] ? L.cf.cm[k] : 0u;
         const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
-        MatchEnv env{nullptr, a.recs + (int64_t)L.wrec[w] * rw, p.cap_from_rec,
-                     a.recs + (int64_t)L.wrec[wb] * rw, ts_base};
-        emit_match<kVm>(a, R, env, key_value(p, kl), seq_base, base + L.v[q] + extra);
+        const CfEnv env{L.cf.wcap[w], 0, p.cap_from_rec, L.cf.wcap[wb],
+                        (int64_t)L.cf.wts[wb] + ts_base};
+        emit_row<kVm>(a, R, env, key_value(p, kl), seq_base + L.wseq[wb], base + L.cf.v[q] + extra);
       }
+      __syncthreads();
+      WALK_STAMP(6);
       // emit carried matches and commit per-key state (lane per key)
       for (int k = tid; k < kpb; k += kWalkThreads) {
         const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
         if (r1 == r0) continue;
         const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
-        uint64_t* blk = a.kstate + kl * (int64_t)p.key_words;
-        uint64_t* sl = blk + 1;
-        const int n0 = (int)(blk[0] & 0xffu);
-        const uint32_t fb = L.firstb[k];
+        uint64_t* sl = a.kslot + (int64_t)bucket * kpb + k;   // slot j word w: sl[(j*sw+w)*ks]
+        const int n0 = (int)(L.khdr[k] & 0xffu);
+        const uint16_t so = L.cf.soff[k];
+        const uint64_t* st = L.cf.sstage + (so != kNone16 ? so : 0);
         if (L.cf.cm[k]) {
-          const uint64_t* brec = a.recs + (int64_t)L.wrec[L.sorted[fb]] * rw;
+          const int wb = L.sorted[L.kcur[k]];
           for (int j = 0; j < L.cf.cm[k]; ++j) {
-            MatchEnv env{sl + (int64_t)(L.cf.cfirst[k] + j) * sw, nullptr, p.cap_from_rec, brec,
-                         ts_base};
-            emit_match<kVm>(a, R, env, key_value(p, kl), seq_base, base + L.v[r0] + j);
+            const int js = L.cf.cfirst[k] + j;
+            const CfEnv env{so != kNone16 ? st + js * sw : sl + (int64_t)js * sw * ks,
+                            so != kNone16 ? 1 : ks, p.cap_from_rec,
+                            L.cf.wcap[wb], (int64_t)L.cf.wts[wb] + ts_base};
+            emit_row<kVm>(a, R, env, key_value(p, kl), seq_base + L.wseq[wb],
+                          base + L.cf.v[r0] + j);
           }
         }
         // survivors: partials created after the last B (all of them if no B),
@@ -934,10 +1010,16 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         int n = 0;
         if (lastb == 0xffffffffu) {   // carried partials survive, minus pruned ones
           for (int j = 0; j < n0; ++j) {
-            const int64_t ets = (int64_t)sl[(int64_t)j * sw];
+            const int64_t ets = so != kNone16 ? (int64_t)st[j * sw] : (int64_t)sl[(int64_t)j * sw * ks];
             if (prune && last_a_ts - ets > p.within) continue;
-            if (n != j)
-              for (int x = 0; x < sw; ++x) sl[(int64_t)n * sw + x] = sl[(int64_t)j * sw + x];
+            if (n != j) {
+              if (so != kNone16) {
+                for (int x = 0; x < sw; ++x) sl[((int64_t)n * sw + x) * ks] = st[j * sw + x];
+              } else {
+                for (int x = 0; x < sw; ++x)
+                  sl[((int64_t)n * sw + x) * ks] = sl[((int64_t)j * sw + x) * ks];
+              }
+            }
             ++n;
           }
         }
@@ -951,22 +1033,24 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
             set_err(a.err, ERR_PENDING);
             break;
           }
-          const uint64_t* rec = a.recs + (int64_t)L.wrec[w] * rw;
-          uint64_t* dst = sl + (int64_t)n * sw;
+          uint64_t* dst = sl + (int64_t)n * sw * ks;
           dst[0] = (uint64_t)ats;
-          dst[1] = (uint64_t)rec_seq(rec, seq_base);
-          for (int c = 0; c < p.ncap; ++c) dst[2 + c] = rec[2 + p.cap_from_rec[c]];
+          dst[ks] = (uint64_t)(seq_base + L.wseq[w]);
+          for (int c = 0; c < p.ncap; ++c) dst[(2 + c) * ks] = L.cf.wcap[w][p.cap_from_rec[c]];
           ++n;
         }
-        blk[0] = (blk[0] & ~0xffull) | (uint64_t)n;
+        const uint32_t nh = (L.khdr[k] & ~0xffu) | (uint32_t)n;
+        L.khdr[k] = nh;
+        a.khdr[(int64_t)bucket * kpb + k] = nh;
       }
       __syncthreads();
+      WALK_STAMP(7);
     } else {
       // ---- general form: one NFA lane per key (count pass, emit pass) -------
       uint32_t mine = 0;
       for (int k = tid; k < kpb; k += kWalkThreads)
         if (L.kstart[k + 1] > L.kstart[k])
-          mine += walk_key<false, kVm>(a, L, R, k, bucket, ts_base, seq_base, 0);
+          mine += walk_key<false, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, 0);
       uint32_t total;
       const uint32_t off = block_excl_scan(mine, L.scratch, &total);
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
@@ -974,7 +1058,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       unsigned long long pos = L.base + off;
       for (int k = tid; k < kpb; k += kWalkThreads)
         if (L.kstart[k + 1] > L.kstart[k])
-          pos += walk_key<true, kVm>(a, L, R, k, bucket, ts_base, seq_base, pos);
+          pos += walk_key<true, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, pos);
       __syncthreads();
     }
     t0 = t1;

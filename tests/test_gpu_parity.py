@@ -234,7 +234,12 @@ def test_pending_overflow_is_reported():
         rt.flush()
 
 
-def test_pending_slots_32_handles_denser_keys():
-    m = pattern_case(workload.PATTERN_PLAN.replace("within 10 sec", "within 4 sec"),
-                     n=30000, keys=256, rate=1, pending_slots=32)
+def test_pending_slots_full_capacity_denser_keys():
+    m = pattern_case(workload.PATTERN_PLAN.replace("within 10 sec", "within 2 sec"),
+                     n=30000, keys=256, rate=1, pending_slots=16)
     assert m > 100
+
+
+def test_pending_slots_above_limit_rejected():
+    with pytest.raises(fs.CepCapacityError):
+        fs.SiddhiAppRuntime(workload.PATTERN_PLAN, pending_slots=32)
