@@ -77,7 +77,13 @@ struct PatternRT {
   PatternArgs pa{};
   DevBuf khdr, kslot;        // per-key state, SoA over the bucket-major key index
   int64_t kstride = 0;       // keys_per_bucket * buckets
-  DevBuf recs, tile_off, chunk_base;
+  // double-buffered chunk arenas: partition(c+1) runs on the side stream
+  // while walk(c) runs on the main stream
+  DevBuf recs[2], tile_off[2], chunk_base[2];
+  hipEvent_t part_done[2] = {nullptr, nullptr}, walk_done[2] = {nullptr, nullptr};
+  PrefPlan pref;               // fast partition path (n < 0: generic)
+  bool used[2] = {false, false};
+  int cur = 0;                 // arena of the next chunk
   int64_t chunk = 0;
   int64_t extra_bound = 0;   // pending partials that may still complete
   bool part_vm = true;       // partition pass needs the interpreter
@@ -95,6 +101,8 @@ struct cep_app {
   CompiledApp app;
   cep_options opt{};
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;    // partition pass of the next chunk
+  hipEvent_t in_ready = nullptr;
   bool enabled = true;
   std::string last_error;
   std::vector<std::string> dict;
@@ -141,18 +149,20 @@ hipEvent_t pool_event(cep_app* a) {
 struct LaunchTimer {
   cep_app* a;
   int kind;
+  hipStream_t st;
   hipEvent_t s = nullptr;
-  LaunchTimer(cep_app* app, int k) : a(app), kind(k) {
+  LaunchTimer(cep_app* app, int k, hipStream_t on = nullptr)
+      : a(app), kind(k), st(on ? on : app->stream) {
     a->launches[k]++;
     if (a->opt.profile) {
       s = pool_event(a);
-      hipEventRecord(s, a->stream);
+      hipEventRecord(s, st);
     }
   }
   ~LaunchTimer() {
     if (a->opt.profile) {
       hipEvent_t e = pool_event(a);
-      hipEventRecord(e, a->stream);
+      hipEventRecord(e, st);
       a->timed.push_back({kind, s, e});
     }
   }
@@ -208,7 +218,9 @@ int create_runtime(cep_app* a) {
   if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
     return fail(a, CEP_E_DEVICE, std::string("libcep is built for gfx950, device is ") +
                                      prop.gcnArchName);
-  if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&a->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&a->in_ready, hipEventDisableTiming) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
@@ -280,7 +292,8 @@ int create_runtime(cep_app* a) {
     rt.kstride = kpb << lg;
     if (!dev_ensure(&rt.khdr, (size_t)rt.kstride * 4, a->stream, false) ||
         !dev_ensure(&rt.kslot, (size_t)rt.kstride * S * p.slot_words * 8, a->stream, false) ||
-        !dev_ensure(&rt.chunk_base, 64, a->stream, false))
+        !dev_ensure(&rt.chunk_base[0], 64, a->stream, false) ||
+        !dev_ensure(&rt.chunk_base[1], 64, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (pattern state)");
     hipMemset(rt.khdr.p, 0, (size_t)rt.kstride * 4);
     int64_t chunk = a->opt.chunk_events;
@@ -289,16 +302,45 @@ int create_runtime(cep_app* a) {
     chunk = (chunk / (kPartThreads * kPartItems)) * (kPartThreads * kPartItems);
     rt.chunk = chunk;
     const int64_t ntiles = chunk / (kPartThreads * kPartItems);
-    if (!dev_ensure(&rt.recs, (size_t)chunk * p.rec_words * 8 + 16, a->stream, false) ||
-        !dev_ensure(&rt.tile_off, (size_t)ntiles * ((1 << lg) + 1) * 2, a->stream, false))
-      return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
+    for (int b = 0; b < 2; ++b) {
+      if (!dev_ensure(&rt.recs[b], (size_t)chunk * p.rec_words * 8 + 16, a->stream, false) ||
+          !dev_ensure(&rt.tile_off[b], (size_t)ntiles * ((1 << lg) + 1) * 2, a->stream, false))
+        return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
+      if (hipEventCreateWithFlags(&rt.part_done[b], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&rt.walk_done[b], hipEventDisableTiming) != hipSuccess)
+        return fail(a, CEP_E_DEVICE, "hipEventCreate failed");
+    }
     rt.extra_bound = (int64_t)S * kc;
     rt.part_vm = (q.f.off >= 0 && q.f_terms.n < 0) || (q.g_raw.off >= 0 && q.g_terms.n < 0);
+    // fast partition path: all columns the pass reads fit kPref registers
+    if (!rt.part_vm && q.key_col_a == q.key_col_b && p.nrec_a <= kPfRec && p.nrec_b <= kPfRec) {
+      PrefPlan& pf = rt.pref;
+      std::vector<int> cols;
+      auto slot = [&](int c) {
+        for (size_t i = 0; i < cols.size(); ++i)
+          if (cols[i] == c) return (int)i;
+        cols.push_back(c);
+        return (int)cols.size() - 1;
+      };
+      pf.key_slot = q.key_col_a >= 0 ? slot(q.key_col_a) : -1;
+      if (q.f.off >= 0)
+        for (int i = 0; i < q.f_terms.n; ++i) pf.f_slot[i] = slot(q.f_terms.t[i].col);
+      if (q.g_raw.off >= 0)
+        for (int i = 0; i < q.g_terms.n; ++i) pf.g_slot[i] = slot(q.g_terms.t[i].col);
+      for (int i = 0; i < p.nrec_a; ++i) pf.reca_slot[i] = slot(p.rec_a[i]);
+      for (int i = 0; i < p.nrec_b; ++i) pf.recb_slot[i] = slot(p.rec_b[i]);
+      if (!cols.empty() && (int)cols.size() <= kPref) {
+        pf.n = (int)cols.size();
+        for (int i = 0; i < kPref; ++i) pf.col[i] = i < pf.n ? cols[i] : cols[0];
+      } else {
+        pf.n = -1;
+      }
+    }
     rt.walk_vm = q.g_in_walk;
     for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
     a->pats.push_back(rt);
   }
-  if (std::getenv("CEP_STAMPS") && !dev_ensure(&a->stamps, (size_t)4096 * 16 * 8, a->stream, false))
+  if (std::getenv("CEP_STAMPS") && !dev_ensure(&a->stamps, (size_t)2 * 4096 * 16 * 8, a->stream, false))
     return fail(a, CEP_E_DEVICE, "out of device memory (stamps)");
   hipStreamSynchronize(a->stream);
   return CEP_OK;
@@ -360,7 +402,16 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
   int rc = ensure_out_cap(a, o, o.bound);
   if (rc) return rc;
   const int P = 1 << rt.pa.buckets_log2;
+  // the side stream starts after everything already queued on the main stream
+  // (host-batch staging copies, earlier queries)
+  hipEventRecord(a->in_ready, a->stream);
+  hipStreamWaitEvent(a->side, a->in_ready, 0);
+  // CEP_NO_OVERLAP=1 (diagnostics): both passes on the main stream
+  static const bool no_overlap = std::getenv("CEP_NO_OVERLAP") != nullptr;
+  hipStream_t side = no_overlap ? a->stream : a->side;
   for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.chunk) {
+    const int b = rt.cur;
+    rt.cur ^= 1;
     RowsArgs rows = rows_all;
     rows.row0 = rows_all.row0 + r0;
     rows.n = std::min<int64_t>(rt.chunk, rows_all.n - r0);
@@ -368,18 +419,38 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     const int64_t ntiles = (rows.n + kPartThreads * kPartItems - 1) / (kPartThreads * kPartItems);
     PartArgs pa{};
     pa.rows = rows;
+    pa.pref = rt.pref;
+    if (pa.pref.n >= 0) {
+      // 16-byte loads need every prefetched column (and ts) 16-byte aligned at
+      // each lane's first row (lanes start at multiples of 8 rows)
+      // (1-byte columns: 8-byte aligned; the hardware takes dword-aligned x4 loads)
+      auto al = [&](const void* p, int w) {
+        const uintptr_t need = w == 1 ? 7u : 15u;
+        return (((uintptr_t)p + (uintptr_t)(rows.row0 * w)) & need) == 0;
+      };
+      bool ok = al(rows.ts, 8) && (!rows.stream || al(rows.stream, 1));
+      for (int i = 0; i < pa.pref.n; ++i) {
+        const int c = pa.pref.col[i];
+        ok = ok && al(rows.cols.p[c], type_width(rows.cols.t[c]));
+      }
+      if (!ok) pa.pref.n = -1;
+    }
     if (r0 > 0) pa.rows.prev_ts = INT64_MIN;
     pa.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
     pa.pat = rt.pa;
     pa.tile_rows = kPartThreads * kPartItems;
-    pa.recs = (uint64_t*)rt.recs.p;
-    pa.tile_off = (uint16_t*)rt.tile_off.p;
-    pa.chunk_base = (int64_t*)rt.chunk_base.p;
+    pa.recs = (uint64_t*)rt.recs[b].p;
+    pa.tile_off = (uint16_t*)rt.tile_off[b].p;
+    pa.chunk_base = (int64_t*)rt.chunk_base[b].p;
     pa.err = (unsigned int*)a->err.p;
+    if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
+    if (rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
     {
-      LaunchTimer t(a, CEP_K_PARTITION);
-      launch_partition(pa, ntiles, rt.part_vm, a->stream);
+      LaunchTimer t(a, CEP_K_PARTITION, side);
+      launch_partition(pa, ntiles, rt.part_vm, side);
     }
+    hipEventRecord(rt.part_done[b], side);
+    hipStreamWaitEvent(a->stream, rt.part_done[b], 0);
     WalkArgs wa{};
     wa.vm = pa.vm;
     wa.pat = rt.pa;
@@ -387,7 +458,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     wa.tile_off = pa.tile_off;
     wa.ntiles = (int)ntiles;
     wa.tile_rows = pa.tile_rows;
-    wa.chunk_base = (const int64_t*)rt.chunk_base.p;
+    wa.chunk_base = (const int64_t*)rt.chunk_base[b].p;
     if (a->stamps.p) {
       // keep the last chunk's stamps (diagnostics only)
       wa.stamps = (uint64_t*)a->stamps.p;
@@ -401,6 +472,8 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
       LaunchTimer t(a, CEP_K_WALK);
       launch_walk(wa, P, rt.walk_vm, a->stream);
     }
+    hipEventRecord(rt.walk_done[b], a->stream);
+    rt.used[b] = true;
   }
   return CEP_OK;
 }
@@ -538,6 +611,16 @@ void cep_destroy(cep_app* a) {
     std::fprintf(stderr, "[cep stamps] k_walk phase ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);
     std::fprintf(stderr, "\n");
+    const int nt = (int)std::min<int64_t>(4096, a->pats[0].chunk / (kPartThreads * kPartItems));
+    std::vector<uint64_t> pt((size_t)nt * 16);
+    hipMemcpy(pt.data(), (uint64_t*)a->stamps.p + 4096 * 16, pt.size() * 8, hipMemcpyDeviceToHost);
+    double ps[16] = {0};
+    for (int b = 0; b < nt; ++b)
+      for (int i = 1; i < 8; ++i)
+        if (pt[b * 16 + i] && pt[b * 16 + i - 1]) ps[i] += (double)(pt[b * 16 + i] - pt[b * 16 + i - 1]);
+    std::fprintf(stderr, "[cep stamps] k_partition phase ticks/block:");
+    for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, ps[i] / nt);
+    std::fprintf(stderr, "\n");
   }
   harvest_timers(a);
   for (auto e : a->event_pool) hipEventDestroy(e);
@@ -550,9 +633,11 @@ void cep_destroy(cep_app* a) {
   for (auto& p : a->pats) {
     dev_free(&p.khdr);
     dev_free(&p.kslot);
-    dev_free(&p.recs);
-    dev_free(&p.tile_off);
-    dev_free(&p.chunk_base);
+    for (int b = 0; b < 2; ++b) {
+      dev_free(&p.recs[b]);
+      dev_free(&p.tile_off[b]);
+      dev_free(&p.chunk_base[b]);
+    }
   }
   for (auto& s : a->stage) dev_free(&s);
   dev_free(&a->code);
@@ -560,6 +645,15 @@ void cep_destroy(cep_app* a) {
   dev_free(&a->tile_state);
   dev_free(&a->ticket);
   dev_free(&a->err);
+  if (a->stream) hipStreamSynchronize(a->stream);
+  if (a->side) hipStreamSynchronize(a->side);
+  for (auto& p : a->pats)
+    for (int b = 0; b < 2; ++b) {
+      if (p.part_done[b]) hipEventDestroy(p.part_done[b]);
+      if (p.walk_done[b]) hipEventDestroy(p.walk_done[b]);
+    }
+  if (a->in_ready) hipEventDestroy(a->in_ready);
+  if (a->side) hipStreamDestroy(a->side);
   if (a->stream) hipStreamDestroy(a->stream);
   delete a;
 }

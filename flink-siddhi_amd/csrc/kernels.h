@@ -94,8 +94,22 @@ struct PatternArgs {
   int32_t closed_form;     // 1: every && g independent of s1 -> data-parallel walk
 };
 
+// Fast partition path: every column the pattern reads (key, f / g term
+// columns, carried columns; at most kPref) is loaded for all of a lane's rows
+// up front with 16-byte loads, so the tile's loads are in flight together.
+constexpr int kPref = 4;
+constexpr int kPfRec = 2;        // carried words per record on the fast path
+struct PrefPlan {
+  int32_t n = -1;                // -1: generic path (per-use loads)
+  int32_t col[kPref];
+  int32_t f_slot[kMaxTerms], g_slot[kMaxTerms];
+  int32_t key_slot = -1;         // -1: unkeyed
+  int32_t reca_slot[8], recb_slot[8];
+};
+
 struct PartArgs {
   RowsArgs rows;
+  PrefPlan pref;
   VmArgs vm;
   PatternArgs pat;
   int32_t from_records;        // 1: input rows are wide records (multi-GPU receive)
@@ -106,6 +120,7 @@ struct PartArgs {
   uint64_t* recs;              // out: records, tile-major
   uint16_t* tile_off;          // out: [ntiles][P+1] exclusive offsets
   int32_t route_world;         // >0: route mode — bucket = owner shard, no key_local
+  uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per tile 16 s_memtime stamps
   unsigned int* err;
 };
 

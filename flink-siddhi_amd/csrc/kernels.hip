@@ -37,6 +37,16 @@ __device__ __forceinline__ void set_err(unsigned int* err, unsigned int bit) {
   if (err) atomicOr(err, bit);
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also releases
+// global memory, which makes every wave drain its outstanding global loads
+// and stores (s_waitcnt vmcnt(0)) before the barrier; phases that only hand
+// LDS data to each other keep their global traffic in flight with this one.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Block-wide exclusive scan of one value per thread (blockDim <= 512).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch /*>=9*/,
                                                     uint32_t* total) {
@@ -49,7 +59,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
     if (lane >= o) x += y;
   }
   if (lane == 63) scratch[wave] = x;
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     uint32_t s = 0;
     for (int w = 0; w < nwaves; ++w) {
@@ -59,10 +69,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
     }
     scratch[8] = s;
   }
-  __syncthreads();
+  lds_barrier();
   uint32_t r = scratch[wave] + x - v;
   *total = scratch[8];
-  __syncthreads();
+  lds_barrier();
   return r;
 }
 
@@ -274,6 +284,72 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) 
   else hipLaunchKernelGGL(k_filter<false>, dim3((unsigned)ntiles), dim3(kFilterThreads), 0, s, a);
 }
 
+
+// ---- fast partition path helpers (PrefPlan) --------------------------------
+// Raw 16-byte loads of E = 8 consecutive rows of a column of width w; branch
+// free (surplus loads repeat the last address), all issued before any use.
+__device__ __forceinline__ void load_raw8(const void* p, int w, int64_t row, uint4 (&r)[4]) {
+  const char* b = (const char*)p + row * w;
+  const int nl = w == 8 ? 4 : (w == 4 ? 2 : 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = gload4(b + 16 * (i < nl ? i : nl - 1));
+}
+
+// Decode 8 rows of raw column data into VM words (load_col semantics).
+__device__ __forceinline__ void decode8(const uint4 (&r)[4], int type, uint64_t (&v)[8]) {
+  const uint32_t x[16] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
+                          r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+  if (type == T_LONG || type == T_DOUBLE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ((uint64_t)x[2 * e + 1] << 32) | x[2 * e];
+  } else if (type == T_BOOL) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ((x[e >> 2] >> (8 * (e & 3))) & 0xffu) ? 1u : 0u;
+  } else if (type == T_FLOAT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (uint64_t)x[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = from_i32((int32_t)x[e]);
+  }
+}
+
+// Value of prefetched slot `slot` (uniform) for row e.
+template <int N>
+__device__ __forceinline__ uint64_t pick(const uint64_t (&v)[kPref][N], int slot, int e) {
+  // masked OR rather than selects: a select chain on slot == q gets rewritten
+  // into a dynamically indexed (scratch) array access
+  uint64_t x = 0;
+#pragma unroll
+  for (int q = 0; q < kPref; ++q) x |= v[q][e] & (0ull - (uint64_t)(slot == q));
+  return x;
+}
+
+// Term-list predicate over prefetched rows (eval_terms_run without loads).
+template <int N>
+__device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const int32_t* slot,
+                                                    const ColSet& cols,
+                                                    const uint64_t (&vals)[kPref][N]) {
+  uint32_t acc = tl.any ? 0u : ((N >= 32) ? 0xffffffffu : ((1u << N) - 1u));
+  for (int i = 0; i < tl.n; ++i) {
+    const Term& t = tl.t[i];
+    uint64_t v[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) v[e] = pick<N>(vals, slot[i], e);
+    int ty = (t.coltype == T_BOOL || t.coltype == T_STRING) ? T_INT : t.coltype;
+    uint32_t nullm = 0;
+    if (t.aop) {
+      convert_run<N>(v, ty, t.atype);
+      arith_run<N>(v, t.aop, t.atype, t.aconst, &nullm);
+      ty = t.atype;
+    }
+    convert_run<N>(v, ty, t.ctype);
+    const uint32_t bits = compare_run<N>(v, t.cop, t.ctype, t.cconst) & ~nullm;
+    acc = tl.any ? (acc | bits) : (acc & bits);
+  }
+  return acc;
+}
+
 // =========================================================== k_partition ==
 // Record layout (8-byte words, chunk-relative):
 //   w0 = dense key (low 32) | role << 32 | input handle << 40
@@ -281,9 +357,16 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) 
 //   w2.. = carried columns (rec_a for A-stream rows, rec_b for B-stream rows)
 // Records of a tile are staged in LDS in bucket order and written out with
 // coalesced 16-byte stores (the tile's region is contiguous).
-constexpr int kStageBytes = 16 * 1024;   // typical tiles keep ~10% of rows
+constexpr int kStageBytes = 32 * 1024;   // a tile keeps ~1/3 of its rows at config 3 (24 B each)
 
-template <bool kVm>
+#define PART_STAMP(i)                                                              \
+  do {                                                                              \
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096)                          \
+      a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)   // typical tiles keep ~10% of rows
+
+// kPf: PrefPlan fast path (term-list predicates, <= kPref columns, aligned).
+template <bool kVm, bool kPf>
 __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   __shared__ uint64_t R[kVm ? kMaxRegs * kPartThreads : 1];
   __shared__ uint32_t scratch[16];
@@ -294,6 +377,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   const PatternArgs& p = a.pat;
   const int P = a.route_world > 0 ? a.route_world : (1 << p.buckets_log2);
   const int rw = p.rec_words;
+  PART_STAMP(0);
   for (int i = tid; i <= P; i += kPartThreads) hist[i] = 0;
 
   // chunk bases: relative seq / ts in records
@@ -309,7 +393,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
     a.chunk_base[0] = ts_base;
     a.chunk_base[1] = seq_base;
   }
-  __syncthreads();
+  lds_barrier();
+  PART_STAMP(1);
 
   constexpr int E = kPartItems;
   const int64_t r0 = tile * (int64_t)a.tile_rows + (int64_t)tid * E;   // first row of this lane
@@ -321,6 +406,10 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   int64_t key[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) key[e] = 0;
+  // fast path: the lane's rows stay in registers for the record build
+  uint64_t tsv[kPf ? E : 1];
+  uint64_t pv[kPf ? kPref : 1][kPf ? E : 1];
+  int sid[kPf ? E : 1];
   if (nvalid > 0) {
     uint32_t role_a = 0, role_b = 0, role_g = 0;
     if (a.from_records) {
@@ -335,6 +424,72 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
           key[e] = (int64_t)(uint32_t)h;
         }
       }
+    } else if constexpr (kPf) {
+      const int64_t row0 = a.rows.row0 + r0;
+      const bool full = nvalid >= 2 * E;   // 16-byte loads of 1-byte columns stay in bounds
+      // issue every load of the lane's rows before any use
+      // (no branches between the loads: a branch join makes the compiler
+      // drain them; unused slots repeat column col[0], set by the host)
+      const int64_t prev_ld = a.rows.ts[row0 > 0 ? row0 - 1 : row0];
+      uint64_t sbytes = 0;
+      if (full) {
+        uint4 rt[4], rc[kPref][4];
+        load_raw8(a.rows.ts, 8, row0, rt);
+#pragma unroll
+        for (int q = 0; q < kPref; ++q)
+          load_raw8(a.rows.cols.p[a.pref.col[q]], type_width(a.rows.cols.t[a.pref.col[q]]), row0,
+                    rc[q]);
+        const uint8_t* sp = a.rows.stream ? a.rows.stream + row0 : (const uint8_t*)a.rows.ts + row0 * 8;
+        sbytes = *(const __attribute__((address_space(1))) uint64_t*)sp;
+        decode8(rt, T_LONG, tsv);
+#pragma unroll
+        for (int q = 0; q < kPref; ++q)
+          if (q < a.pref.n) decode8(rc[q], a.rows.cols.t[a.pref.col[q]], pv[q]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          tsv[e] = e < nvalid ? (uint64_t)a.rows.ts[row0 + e] : 0;
+          if (a.rows.stream && e < nvalid) sbytes |= (uint64_t)a.rows.stream[row0 + e] << (8 * e);
+#pragma unroll
+          for (int q = 0; q < kPref; ++q)
+            pv[q][e] = (q < a.pref.n && e < nvalid)
+                           ? load_col(a.rows.cols.p[a.pref.col[q]], a.rows.cols.t[a.pref.col[q]], row0 + e)
+                           : 0;
+        }
+      }
+      int64_t prev = row0 > 0 ? prev_ld : a.rows.prev_ts;
+      uint32_t is_a = 0, is_b = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        sid[e] = a.rows.stream ? (int)((sbytes >> (8 * e)) & 0xffu) : a.rows.input;
+        if (e < nvalid) {
+          is_a |= (sid[e] == p.a_stream ? 1u : 0u) << e;
+          is_b |= (sid[e] == p.b_stream ? 1u : 0u) << e;
+        }
+      }
+      if (p.within >= 0) {   // event-time order check (`within` pruning relies on it)
+        bool bad = false;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (e < nvalid) {
+            bad |= (int64_t)tsv[e] < prev;
+            prev = (int64_t)tsv[e];
+          }
+        }
+        if (bad) set_err(a.err, ERR_ORDER);
+      }
+      const uint32_t all = (1u << E) - 1u;
+      if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
+      if (is_b) {
+        if (p.g_walk_prog >= 0) {
+          role_b = is_b;
+        } else {
+          role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
+          role_g = role_b;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) key[e] = a.pref.key_slot >= 0 ? (int64_t)pick<E>(pv, a.pref.key_slot, e) : 0;
     } else {
       const int64_t row0 = a.rows.row0 + r0;
       uint32_t is_a = 0, is_b = 0;
@@ -415,7 +570,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       packed[e] = ((uint32_t)bucket << 14) | (role << 11) | rank;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  PART_STAMP(2);
   // exclusive scan of the P bucket counts (P <= 4096: 16 per thread); every
   // thread of the block takes part (barriers inside)
   {
@@ -437,40 +593,67 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       }
       if (tid == 0) hist[P] = total;
   }
-  __syncthreads();
+  lds_barrier();
+  PART_STAMP(3);
   const bool staged = (int64_t)hist[P] * rw * 8 <= kStageBytes;   // uniform
   {
     // build the records (LDS stage when they fit, else straight to HBM)
     const int64_t tbase = tile * (int64_t)a.tile_rows;
+    const int sa0 = a.pref.reca_slot[0], sa1 = a.pref.reca_slot[1];
+    const int sb0 = a.pref.recb_slot[0], sb1 = a.pref.recb_slot[1];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       if (packed[e] == 0xffffffffu) continue;
       const uint32_t b = packed[e] >> 14, rank = packed[e] & 0x7ffu;
       const uint32_t role = (packed[e] >> 11) & 7u;
       const uint32_t slot = hist[b] + rank;
-      uint64_t* out = staged ? stage + (int64_t)slot * rw : a.recs + (tbase + slot) * rw;
+      // explicit address spaces (a generic pointer would make these flat stores)
+      const int64_t so = (int64_t)slot * rw;
+      uint64_t* gout = a.recs + (tbase + slot) * rw;
+      auto put = [&](int w, uint64_t v) {
+        if (staged) stage[so + w] = v;
+        else gout[w] = v;
+      };
       const int64_t r = a.rows.row0 + r0 + e;
-      if (a.from_records) {
-        const uint64_t* in = a.in_recs + r * a.in_rec_words;
-        out[0] = (in[0] & ~0xffffffffull) | (uint64_t)(uint32_t)key[e];
-        out[1] = (uint64_t)(uint32_t)((int64_t)in[1] - seq_base) |
-                 ((uint64_t)(uint32_t)(int32_t)((int64_t)in[2] - ts_base) << 32);
-        for (int w = 2; w < rw; ++w) out[w] = in[w + 1];
-        continue;
+      if constexpr (!kPf) {
+        if (a.from_records) {
+          const uint64_t* in = a.in_recs + r * a.in_rec_words;
+          put(0, (in[0] & ~0xffffffffull) | (uint64_t)(uint32_t)key[e]);
+          put(1, (uint64_t)(uint32_t)((int64_t)in[1] - seq_base) |
+                   ((uint64_t)(uint32_t)(int32_t)((int64_t)in[2] - ts_base) << 32));
+          for (int w = 2; w < rw; ++w) put(w, in[w + 1]);
+          continue;
+        }
       }
-      const int s = a.rows.stream ? (int)a.rows.stream[r] : a.rows.input;
-      const int64_t dts = a.rows.ts[r] - ts_base;
+      int s;
+      int64_t dts;
+      if constexpr (kPf) {
+        s = sid[e];
+        dts = (int64_t)tsv[e] - ts_base;
+      } else {
+        s = a.rows.stream ? (int)a.rows.stream[r] : a.rows.input;
+        dts = a.rows.ts[r] - ts_base;
+      }
       if (dts > 0x7fffffffll || dts < -0x7fffffffll) set_err(a.err, ERR_ORDER);
-      out[0] = (uint64_t)(uint32_t)key[e] | ((uint64_t)role << 32) | ((uint64_t)(uint32_t)s << 40);
-      out[1] = (uint64_t)(uint32_t)(r - a.rows.row0) | ((uint64_t)(uint32_t)(int32_t)dts << 32);
-      const int nrc = s == p.a_stream ? p.nrec_a : p.nrec_b;
-      for (int c = 0; c < nrc; ++c) {
-        const int col = s == p.a_stream ? p.rec_a[c] : p.rec_b[c];
-        out[2 + c] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], r);
+      put(0, (uint64_t)(uint32_t)key[e] | ((uint64_t)role << 32) | ((uint64_t)(uint32_t)s << 40));
+      put(1, (uint64_t)(uint32_t)(r - a.rows.row0) | ((uint64_t)(uint32_t)(int32_t)dts << 32));
+      const bool isa = s == p.a_stream;
+      if constexpr (kPf) {
+        // at most kPfRec carried words (host-checked); slots are uniform
+        const int nrc = isa ? p.nrec_a : p.nrec_b;
+        if (nrc > 0) put(2, pick<E>(pv, isa ? sa0 : sb0, e));
+        if (nrc > 1) put(3, pick<E>(pv, isa ? sa1 : sb1, e));
+      } else {
+        const int nrc = isa ? p.nrec_a : p.nrec_b;
+        for (int c = 0; c < nrc; ++c) {
+          const int col = isa ? p.rec_a[c] : p.rec_b[c];
+          put(2 + c, load_col(a.rows.cols.p[col], a.rows.cols.t[col], r));
+        }
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
+  PART_STAMP(4);
   uint16_t* toff = a.tile_off + tile * (int64_t)(P + 1);
   for (int i = tid; i <= P; i += kPartThreads) toff[i] = (uint16_t)hist[i];
   if (staged) {
@@ -485,13 +668,17 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       }
     }
   }
+  lds_barrier();
+  PART_STAMP(5);
 }
 
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s) {
   const int P = a.route_world > 0 ? a.route_world : (1 << a.pat.buckets_log2);
   const size_t dyn = ((size_t)(P + 1) * 4 + 15) & ~(size_t)15;
-  if (vm) hipLaunchKernelGGL(k_partition<true>, dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
-  else hipLaunchKernelGGL(k_partition<false>, dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
+  if (vm) hipLaunchKernelGGL((k_partition<true, false>), dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
+  else if (a.pref.n >= 0 && !a.from_records)
+    hipLaunchKernelGGL((k_partition<false, true>), dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
+  else hipLaunchKernelGGL((k_partition<false, false>), dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
 }
 
 // ================================================================ k_walk ==
@@ -778,7 +965,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     }
     if (tid == 0) L.seg[ntiles] = total;
   }
-  __syncthreads();
+  lds_barrier();
   WALK_STAMP(1);
 
   int t0 = 0;
@@ -796,7 +983,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       L.t1 = (uint32_t)lo;
     }
     for (int k = tid; k <= kpb; k += kWalkThreads) L.kstart[k] = 0;
-    __syncthreads();
+    lds_barrier();
     const int t1 = (int)L.t1;
     const uint32_t wbase = L.seg[t0];
     const uint32_t nrec = L.seg[t1] - wbase;
@@ -811,7 +998,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       const uint32_t g0 = (uint32_t)t * (uint32_t)a.tile_rows + L.lo[t];
       for (uint32_t j = 0; j < cnt && pos + j < (uint32_t)kWalkWindow; ++j) L.wrec[pos + j] = g0 + j;
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t w = tid; w < nw; w += kWalkThreads) {
       const uint64_t* rec = a.recs + (int64_t)L.wrec[w] * rw;
       const uint4 hv = gload4(rec);   // w0, w1 in one 16-byte load
@@ -828,7 +1015,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       }
       atomicAdd(&L.kstart[((uint32_t)h >> p.buckets_log2) + 1], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     WALK_STAMP(2);
     // exclusive scan of key counts (kstart[1..kpb] -> kstart[0..kpb])
     {
@@ -842,12 +1029,12 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       }
       if (tid == 0) L.kstart[kpb] = total;
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t w = tid; w < nw; w += kWalkThreads) {
       const uint32_t slot = atomicAdd(&L.kcur[L.wkey[w]], 1u);
       L.sorted[slot] = (uint16_t)w;
     }
-    __syncthreads();
+    lds_barrier();
     // restore arrival order inside each key run (insertion / shell sort on seq)
     for (int k = tid; k < kpb; k += kWalkThreads) {
       const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
@@ -867,7 +1054,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         if (gap == 1) break;
       }
     }
-    __syncthreads();
+    lds_barrier();
     WALK_STAMP(3);
 
     if (p.closed_form) {
@@ -897,7 +1084,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
       for (int k = tid; k < kpb; k += kWalkThreads) {
         const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
         uint32_t nb = 0xffffffffu;
@@ -928,7 +1115,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         L.cf.cm[k] = cm;
         L.cf.cfirst[k] = cf;
       }
-      __syncthreads();
+      lds_barrier();
       WALK_STAMP(4);
       // per-position match flag + carried count at run start -> scan input
       constexpr int per = kWalkWindow / kWalkThreads;   // 2 contiguous positions per lane
@@ -958,7 +1145,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         off += vals[i];
       }
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
-      __syncthreads();
+      lds_barrier();
       WALK_STAMP(5);
       const unsigned long long base = L.base;
       // emit record matches (lane per position; record words in LDS: stores only)
@@ -975,7 +1162,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
                         (int64_t)L.cf.wts[wb] + ts_base};
         emit_row<kVm>(a, R, env, key_value(p, kl), seq_base + L.wseq[wb], base + L.cf.v[q] + extra);
       }
-      __syncthreads();
+      // (no barrier: the commit below reads nothing the emission writes)
       WALK_STAMP(6);
       // emit carried matches and commit per-key state (lane per key)
       for (int k = tid; k < kpb; k += kWalkThreads) {
@@ -1043,7 +1230,6 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
         L.khdr[k] = nh;
         a.khdr[(int64_t)bucket * kpb + k] = nh;
       }
-      __syncthreads();
       WALK_STAMP(7);
     } else {
       // ---- general form: one NFA lane per key (count pass, emit pass) -------
@@ -1054,13 +1240,15 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       uint32_t total;
       const uint32_t off = block_excl_scan(mine, L.scratch, &total);
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
-      __syncthreads();
+      lds_barrier();
       unsigned long long pos = L.base + off;
       for (int k = tid; k < kpb; k += kWalkThreads)
         if (L.kstart[k + 1] > L.kstart[k])
           pos += walk_key<true, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, pos);
-      __syncthreads();
     }
+    // the next window re-reads state slots this one wrote (HBM) and reuses
+    // the LDS arrays: full barrier; none after the last window
+    if (t1 < ntiles) __syncthreads();
     t0 = t1;
   }
 }
