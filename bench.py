@@ -46,20 +46,35 @@ def parse():
     ap.add_argument("--chunk", type=int, default=1 << 22)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--ingest", choices=["shuffle", "prepartitioned"], default="shuffle",
+                    help="multi-GPU pattern input: engine key shuffle over RCCL, or keyed upstream")
     return ap.parse_args()
 
 
 def dist_init(args):
+    """One process per GPU.  CEP_DIST_BACKEND=gloo (rehearsal on a box with
+    fewer GPUs than ranks: ranks share devices, exchanges staged via host)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    backend = os.environ.get("CEP_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
+
+
+def _coll_device():
+    import torch.distributed as dist
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
 
 
 def barrier(world):
@@ -73,7 +88,7 @@ def max_over_ranks(world, v: float) -> float:
         return v
     import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -83,9 +98,31 @@ def sum_over_ranks(world, v: float) -> float:
         return v
     import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64, device=_coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (scripts/gpu_pmc.sh -> scripts/pmc_summary.py -> profiles/r01_pmc.json;
+    FETCH_SIZE doubled per the gfx950 caveat).  Measured in separate
+    rocprofv3 --pmc passes of this same bench command; null if absent."""
+    import glob
+    import json as _json
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = _json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d and "hbm_bytes_per_launch" in d[kernel]:
+            return {"bytes_per_launch": round(d[kernel]["hbm_bytes_per_launch"]),
+                    "read": round(d[kernel]["hbm_read_bytes"]),
+                    "write": round(d[kernel]["hbm_write_bytes"]),
+                    "source": os.path.relpath(f, os.path.dirname(os.path.abspath(__file__)))}
+    return None
 
 
 def cpu_baseline_pattern(args, budget_s):
@@ -156,20 +193,38 @@ def main():
     # Inputs for every step, generated on the device before the timed region.
     # Multi-GPU: rank r's events are the ones whose key it owns (the result of
     # the keyBy shuffle), drawn from its own contiguous index ranges.
+    # Multi-GPU ingest: "shuffle" (default) — rank r holds global index range
+    # r of each step and the engine routes it (push-down + owner = k % world),
+    # RCCL all-to-all moves the records, each owner walks what it received;
+    # "prepartitioned" — the input is already keyed upstream (Flink keyBy):
+    # rank r draws only keys it owns, no exchange.
+    shuffle_mode = pattern and world > 1 and args.ingest == "shuffle"
     batches = []
     for s in range(warm + steps):
         first = (s * world + rank) * n
         d = workload.generate_device(first, n, args.keys, rate=args.rate,
                                      single_stream=not pattern, device="cuda")
-        if pattern and world > 1:
+        d["first"] = first
+        if pattern and world > 1 and not shuffle_mode:
             d["k"] = (d["k"] // world) * world + rank     # owned keys, same distribution
         if not pattern:
             d["name"] = torch.zeros(n, dtype=torch.int32, device="cuda")
         batches.append(d)
     torch.cuda.synchronize()
 
+    bufs = {}
+
     def step(d):
-        if pattern:
+        if shuffle_mode:
+            from flink_siddhi import shuffle
+            recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
+                                    world, seq0=d["first"], streams=d["stream"],
+                                    out=bufs.get("send"))
+            bufs["send"] = recs
+            recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get("recv"))
+            bufs["recv"] = recv
+            rt.send_records(recv, m, n)
+        elif pattern:
             rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
         else:
             rt.send("inputStream", d["ts"], [d["id"], d["name"], d["price"], d["ts"]])
@@ -194,26 +249,34 @@ def main():
 
     # per-kernel HIP-event times on the engine's stream over the timed region
     kern = {}
-    for k, name in ((L.K_PARTITION, "k_partition"), (L.K_WALK, "k_walk"), (L.K_FILTER, "k_filter")):
+    for k, name in ((L.K_PARTITION, "k_partition"), (L.K_WALK, "k_walk"), (L.K_FILTER, "k_filter"),
+                    (L.K_ROUTE, "k_route")):
         launches = st1.kernel_launches[k] - st0.kernel_launches[k]
         ms = st1.kernel_ms[k] - st0.kernel_ms[k]
         if launches:
             kern[name] = {"launches": int(launches), "avg_us": 1e3 * ms / launches,
                           "total_ms": ms}
-    dom = max(kern, key=lambda k: kern[k]["total_ms"])
     m_per_event = (st1.matches_out - st0.matches_out) / float(n * steps)
     if pattern:
         chunk_events = min(args.chunk, n)
-        per_launch = {"k_partition": PATTERN_IN_BYTES * chunk_events,
-                      "k_walk": PATTERN_OUT_BYTES * m_per_event * chunk_events}
+        walk_launches = kern.get("k_walk", {}).get("launches", 0)
+        per_launch = {"k_walk": PATTERN_OUT_BYTES * (st1.matches_out - st0.matches_out) /
+                      max(1, walk_launches)}
+        if shuffle_mode:
+            # route reads the whole step batch once; the owner's partition pass
+            # then reads records, not events (its bytes are not attributed here)
+            per_launch["k_route"] = PATTERN_IN_BYTES * n
+        else:
+            per_launch["k_partition"] = PATTERN_IN_BYTES * chunk_events
         alg_per_event = PATTERN_IN_BYTES + PATTERN_OUT_BYTES * m_per_event
     else:
         per_launch = {"k_filter": (FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event) * n}
         alg_per_event = FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event
+    dom = max((k for k in kern if k in per_launch), key=lambda k: kern[k]["total_ms"])
     achieved = per_launch[dom] / (kern[dom]["avg_us"] * 1e-6) / 1e9
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": pmc_traffic(dom) if world == 1 else None,
                 "bytes_per_launch": per_launch[dom], "avg_launch_us": round(kern[dom]["avg_us"], 2)}
     per_gpu_events = value / world
     pipeline = {"alg_bytes_per_event": round(alg_per_event, 3),
@@ -234,7 +297,11 @@ def main():
             "dtype": "f64+int32+int64", "data": "synthetic (splitmix64 counter stream, BASELINE.md §3)",
             "config": ({"workload": "config3: keyed every A -> B within 10 sec, partition with k",
                         "keys": args.keys, "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
-                        "chunk_events": args.chunk, "parallelism": "key-sharded x%d" % world}
+                        "chunk_events": args.chunk, "parallelism": "key-sharded x%d" % world,
+                        "ingest": (("%s all-to-all key shuffle" % ("rccl" if _coll_device() == "cuda"
+                                                                    else "gloo host-staged"))
+                                    if shuffle_mode else
+                                   "pre-partitioned (keyed upstream)") if world > 1 else "local"}
                        if pattern else
                        {"workload": "config2: inputStream[price > 0.5 and id % 7 == 0] select *",
                         "events_per_step_per_gpu": n, "parallelism": "replicas x%d" % world}),

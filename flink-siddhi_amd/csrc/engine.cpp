@@ -111,6 +111,7 @@ struct cep_app {
   std::vector<OutStream> outs;
   std::vector<PatternRT> pats;
   DevBuf tile_state, ticket, err;
+  DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   std::vector<DevBuf> stage;   // host-batch staging columns (+ts, +stream)
   int64_t events_in = 0, matches_out = 0, batches = 0;
@@ -394,7 +395,8 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
   return CEP_OK;
 }
 
-int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
+int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
+                const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
   const Query& q = a->app.queries[rt.q];
   OutStream& o = a->outs[a->app.output_index(q.out_stream)];
   if (o.bound == 0) o.bound = rt.extra_bound;
@@ -420,6 +422,12 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all) {
     PartArgs pa{};
     pa.rows = rows;
     pa.pref = rt.pref;
+    if (in_recs) {   // received shuffle records (cep_send_records)
+      pa.from_records = 1;
+      pa.in_recs = in_recs;
+      pa.in_rec_words = in_rec_words;
+      pa.pref.n = -1;
+    }
     if (pa.pref.n >= 0) {
       // 16-byte loads need every prefetched column (and ts) 16-byte aligned at
       // each lane's first row (lanes start at multiples of 8 rows)
@@ -643,6 +651,10 @@ void cep_destroy(cep_app* a) {
   dev_free(&a->code);
   dev_free(&a->konst);
   dev_free(&a->tile_state);
+  dev_free(&a->route_arena);
+  dev_free(&a->route_tcount);
+  dev_free(&a->route_toffs);
+  dev_free(&a->route_dcount);
   dev_free(&a->ticket);
   dev_free(&a->err);
   if (a->stream) hipStreamSynchronize(a->stream);
@@ -684,11 +696,12 @@ int cep_set_callback(cep_app* a, const char* out_id, cep_emit_fn fn, void* user)
   return CEP_OK;
 }
 
-int cep_send_batch(cep_app* a, const cep_batch* b) {
-  if (!a || !b) return CEP_E_ARG;
-  if (!a->enabled) return CEP_OK;   // AbstractSiddhiOperator.java:128
+namespace {
+
+// Batch -> device rows (host batches are staged into device memory: the
+// PCIe-inclusive path).  Validates the handle and the column count.
+int batch_rows(cep_app* a, const cep_batch* b, RowsArgs* out) {
   if (b->n < 0 || (b->n > 0 && !b->ts)) return fail(a, CEP_E_ARG, "bad batch");
-  if (b->n == 0) return CEP_OK;
   if (b->input < 0 || b->input >= (int)a->app.inputs.size())
     return fail(a, CEP_E_UNDEFINED_STREAM, "undefined input handle");
   const StreamSchema& sd = a->app.inputs[b->input];
@@ -707,8 +720,10 @@ int cep_send_batch(cep_app* a, const cep_batch* b) {
     for (int c = 0; c < b->ncols; ++c) rows.cols.p[c] = b->cols[c];
     rows.ts = b->ts;
     rows.stream = b->stream;
+    // cross-batch order checks would need a sync to read the last ts; the
+    // in-batch check covers the hot path
+    a->last_ts = INT64_MIN;
   } else {
-    // host batch: stage into device memory (the PCIe-inclusive path)
     size_t need = (size_t)b->ncols + 2;
     if (a->stage.size() < need) a->stage.resize(need);
     for (int c = 0; c < b->ncols; ++c) {
@@ -732,14 +747,22 @@ int cep_send_batch(cep_app* a, const cep_batch* b) {
     }
     a->last_ts = b->ts[b->n - 1];
   }
-  if (b->on_device) {
-    // last ts for cross-batch order checks: read the final element asynchronously
-    // is not worth a sync; the in-batch check covers the hot path.
-    a->last_ts = INT64_MIN;
-  }
+  *out = rows;
+  return CEP_OK;
+}
+
+}  // namespace
+
+int cep_send_batch(cep_app* a, const cep_batch* b) {
+  if (!a || !b) return CEP_E_ARG;
+  if (!a->enabled) return CEP_OK;   // AbstractSiddhiOperator.java:128
+  if (b->n == 0) return CEP_OK;
+  RowsArgs rows{};
+  int rc = batch_rows(a, b, &rows);
+  if (rc) return rc;
   a->events_in += b->n;
   a->batches++;
-  int rc = send_device_rows(a, rows);
+  rc = send_device_rows(a, rows);
   if (b->on_device == 0) hipStreamSynchronize(a->stream);   // host buffers may be reused
   return rc;
 }
@@ -997,18 +1020,78 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
 
 int cep_record_words(cep_app* a) {
   if (!a || a->pats.size() != 1) return -CEP_E_UNSUPPORTED;
-  return a->pats[0].pa.rec_words;
+  return a->pats[0].pa.rec_words + 1;   // wide record: [hdr, seq, ts, carried...]
 }
 
-int cep_route_batch(cep_app* a, const cep_batch* b, int world, void* rec_out, int64_t rec_cap,
-                    int64_t* counts_host) {
-  (void)a; (void)b; (void)world; (void)rec_out; (void)rec_cap; (void)counts_host;
-  return CEP_E_UNSUPPORTED;
+int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out,
+                    int64_t rec_cap, int64_t* counts_host) {
+  if (!a || !b || !counts_host || world <= 0) return CEP_E_ARG;
+  if (world > kMaxWorld) return fail(a, CEP_E_ARG, "world exceeds " + std::to_string(kMaxWorld));
+  if (a->pats.size() != 1 || a->app.queries.size() != 1)
+    return fail(a, CEP_E_UNSUPPORTED, "key shuffle needs an app with exactly one keyed pattern");
+  PatternRT& rt = a->pats[0];
+  const Query& q = a->app.queries[rt.q];
+  if (q.key_col_a < 0 || q.key_col_b < 0)
+    return fail(a, CEP_E_UNSUPPORTED, "key shuffle needs a partitioned pattern");
+  for (int d = 0; d < world; ++d) counts_host[d] = 0;
+  if (b->n == 0) return CEP_OK;
+  RowsArgs rows{};
+  int rc = batch_rows(a, b, &rows);
+  if (rc) return rc;
+  const int64_t tile_rows = kPartThreads * kPartItems;
+  const int64_t ntiles = (b->n + tile_rows - 1) / tile_rows;
+  const int wrw = rt.pa.rec_words + 1;
+  if (!dev_ensure(&a->route_arena, (size_t)ntiles * tile_rows * wrw * 8, a->stream, false) ||
+      !dev_ensure(&a->route_tcount, (size_t)ntiles * world * 4, a->stream, false) ||
+      !dev_ensure(&a->route_toffs, (size_t)ntiles * world * 4, a->stream, false) ||
+      !dev_ensure(&a->route_dcount, (size_t)world * 8, a->stream, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory (route arena)");
+  RouteArgs ra{};
+  ra.rows = rows;
+  ra.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
+  ra.pat = rt.pa;
+  ra.world = world;
+  ra.wrw = wrw;
+  ra.tile_rows = (int32_t)tile_rows;
+  ra.seq0 = seq0;
+  ra.arena = (uint64_t*)a->route_arena.p;
+  ra.tcount = (uint32_t*)a->route_tcount.p;
+  ra.err = (unsigned int*)a->err.p;
+  {
+    LaunchTimer t(a, CEP_K_ROUTE);
+    launch_route(ra, ntiles, rt.part_vm, (uint32_t*)a->route_toffs.p,
+                 (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
+  }
+  // counts first: the gather must not overrun rec_out
+  std::vector<unsigned long long> dc(world);
+  hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, a->stream);
+  if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "route failed");
+  int64_t total = 0;
+  for (int d = 0; d < world; ++d) {
+    counts_host[d] = (int64_t)dc[d];
+    total += (int64_t)dc[d];
+  }
+  if (total > rec_cap) return fail(a, CEP_E_CAPACITY, "rec_out holds fewer records than routed");
+  rc = check_device_error(a);
+  if (rc) return rc;
+  a->batches++;
+  return CEP_OK;
 }
 
 int cep_send_records(cep_app* a, const void* recs, int64_t n, int64_t events_represented) {
-  (void)a; (void)recs; (void)n; (void)events_represented;
-  return CEP_E_UNSUPPORTED;
+  if (!a || (n > 0 && !recs) || n < 0) return CEP_E_ARG;
+  if (!a->enabled) return CEP_OK;
+  if (a->pats.size() != 1 || a->app.queries.size() != 1)
+    return fail(a, CEP_E_UNSUPPORTED, "records need an app with exactly one keyed pattern");
+  a->events_in += events_represented;
+  if (n == 0) return CEP_OK;
+  PatternRT& rt = a->pats[0];
+  RowsArgs rows{};
+  rows.n = n;
+  rows.row0 = 0;
+  rows.input = rt.pa.a_stream;
+  a->batches++;
+  return run_pattern(a, rt, rows, (const uint64_t*)recs, rt.pa.rec_words + 1);
 }
 
 int cep_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys, int64_t rate, int64_t t0,

@@ -119,8 +119,22 @@ struct PartArgs {
   int32_t tile_rows;           // rows per tile (2048)
   uint64_t* recs;              // out: records, tile-major
   uint16_t* tile_off;          // out: [ntiles][P+1] exclusive offsets
-  int32_t route_world;         // >0: route mode — bucket = owner shard, no key_local
   uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per tile 16 s_memtime stamps
+  unsigned int* err;
+};
+
+// Multi-GPU key shuffle (sender side).
+constexpr int kMaxWorld = 64;
+struct RouteArgs {
+  RowsArgs rows;
+  VmArgs vm;
+  PatternArgs pat;
+  int32_t world;               // owners: key % world
+  int32_t wrw;                 // wide record words: 3 + max(nrec_a, nrec_b)
+  int32_t tile_rows;
+  int64_t seq0;                // global arrival number of batch row 0
+  uint64_t* arena;             // [ntiles][tile_rows * wrw], owner-grouped per tile
+  uint32_t* tcount;            // [ntiles][world] kept rows per owner
   unsigned int* err;
 };
 
@@ -147,6 +161,8 @@ struct WalkArgs {
 // --------------------------------------------------------------- launchers --
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
+void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
+                  unsigned long long* dcount, uint64_t* out, hipStream_t s);
 void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s);
 void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
                      int64_t rate, int64_t t0, int single_stream, int32_t* key,

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   const int tid = threadIdx.x;
   const int64_t tile = blockIdx.x;
   const PatternArgs& p = a.pat;
-  const int P = a.route_world > 0 ? a.route_world : (1 << p.buckets_log2);
+  const int P = 1 << p.buckets_log2;
   const int rw = p.rec_words;
   PART_STAMP(0);
   for (int i = tid; i <= P; i += kPartThreads) hist[i] = 0;
@@ -549,21 +549,13 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
                             ((role_g >> e) & 1u) * ROLE_G;
       if (!role) continue;
-      int bucket;
-      int64_t kfield;
-      if (a.route_world > 0) {
-        if (key[e] < 0) { set_err(a.err, ERR_KEY_RANGE); continue; }
-        bucket = (int)(key[e] % a.route_world);
-        kfield = key[e];
-      } else {
-        if (key[e] < 0 || (key[e] % p.key_stride) != p.key_offset) {
-          set_err(a.err, ERR_KEY_RANGE);
-          continue;
-        }
-        kfield = key[e] / p.key_stride;
-        if (kfield >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
-        bucket = (int)(kfield & (P - 1));
+      if (key[e] < 0 || (key[e] % p.key_stride) != p.key_offset) {
+        set_err(a.err, ERR_KEY_RANGE);
+        continue;
       }
+      const int64_t kfield = key[e] / p.key_stride;
+      if (kfield >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
+      const int bucket = (int)(kfield & (P - 1));
       key[e] = kfield;
       const uint32_t rank = atomicAdd(&hist[bucket], 1u);
       // bits 0-10 rank in tile, 11-13 role, 14-25 bucket
@@ -618,6 +610,9 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       if constexpr (!kPf) {
         if (a.from_records) {
           const uint64_t* in = a.in_recs + r * a.in_rec_words;
+          const int64_t dseq = (int64_t)in[1] - seq_base, dts = (int64_t)in[2] - ts_base;
+          if (dseq < 0 || dseq > 0xffffffffll || dts > 0x7fffffffll || dts < -0x7fffffffll)
+            set_err(a.err, ERR_ORDER);
           put(0, (in[0] & ~0xffffffffull) | (uint64_t)(uint32_t)key[e]);
           put(1, (uint64_t)(uint32_t)((int64_t)in[1] - seq_base) |
                    ((uint64_t)(uint32_t)(int32_t)((int64_t)in[2] - ts_base) << 32));
@@ -673,12 +668,161 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
 }
 
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s) {
-  const int P = a.route_world > 0 ? a.route_world : (1 << a.pat.buckets_log2);
+  const int P = 1 << a.pat.buckets_log2;
   const size_t dyn = ((size_t)(P + 1) * 4 + 15) & ~(size_t)15;
   if (vm) hipLaunchKernelGGL((k_partition<true, false>), dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
   else if (a.pref.n >= 0 && !a.from_records)
     hipLaunchKernelGGL((k_partition<false, true>), dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
   else hipLaunchKernelGGL((k_partition<false, false>), dim3((unsigned)ntiles), dim3(kPartThreads), dyn, s, a);
+}
+
+
+// ============================================================== k_route ==
+// Multi-GPU key shuffle, sender side (router/HashPartitioner.java:24-26:
+// owner = abs(hashCode(key)) % n; for the engine's non-negative int keys that
+// is key % world).  Predicates are pushed down (rows no state
+// can use never leave the GPU).  Each tile writes its kept rows as wide
+// records [hdr, seq, ts, carried...] grouped by owner, in arrival order (one
+// block scan per owner gives stable ranks); k_route_scan / k_route_gather
+// then concatenate every owner's segments over tiles into one contiguous run.
+template <bool kVm>
+__global__ __launch_bounds__(kPartThreads) void k_route(RouteArgs a) {
+  __shared__ uint64_t R[kVm ? kMaxRegs * kPartThreads : 1];
+  __shared__ uint32_t scratch[16];
+  __shared__ uint32_t dbase[kMaxWorld + 1];
+  const int tid = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  const PatternArgs& p = a.pat;
+  constexpr int E = kPartItems;
+  const int64_t r0 = tile * (int64_t)a.tile_rows + (int64_t)tid * E;
+  const int64_t nvalid = a.rows.n - r0;
+  const int64_t row0 = a.rows.row0 + r0;
+  uint32_t role_a = 0, role_b = 0, role_g = 0;
+  int sid[E];
+  int64_t key[E];
+  int dest[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    key[e] = 0;
+    dest[e] = -1;
+    sid[e] = -1;
+  }
+  if (nvalid > 0) {
+    uint32_t is_a = 0, is_b = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      sid[e] = a.rows.stream ? (e < nvalid ? (int)a.rows.stream[row0 + e] : -1) : a.rows.input;
+      if (e < nvalid) {
+        is_a |= (sid[e] == p.a_stream ? 1u : 0u) << e;
+        is_b |= (sid[e] == p.b_stream ? 1u : 0u) << e;
+      }
+    }
+    if (is_a) role_a = is_a & eval_run<E, kVm>(p.f_terms, a.vm, p.f_prog, R, a.rows, row0, nvalid);
+    if (is_b) {
+      if (p.g_walk_prog >= 0) {
+        role_b = is_b;
+      } else {
+        role_b = is_b & eval_run<E, kVm>(p.g_terms, a.vm, p.g_raw_prog, R, a.rows, row0, nvalid);
+        role_g = role_b;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (!(((role_a | role_b) >> e) & 1u)) continue;
+      const int kc = sid[e] == p.a_stream ? p.key_col_a : p.key_col_b;
+      key[e] = kc >= 0 ? (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e) : 0;
+      if (key[e] < 0 || key[e] > 0xffffffffll) {
+        set_err(a.err, ERR_KEY_RANGE);
+        continue;
+      }
+      dest[e] = (int)(key[e] % a.world);
+    }
+  }
+  // stable per-owner ranks: one block scan per owner
+  uint32_t rank[E];
+  for (int d = 0; d < a.world; ++d) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) c += dest[e] == d ? 1u : 0u;
+    uint32_t total;
+    uint32_t off = block_excl_scan(c, scratch, &total);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (dest[e] == d) rank[e] = off++;
+    if (tid == 0) {
+      dbase[d] = d == 0 ? 0u : dbase[d - 1] + a.tcount[tile * a.world + d - 1];
+      a.tcount[tile * a.world + d] = total;
+    }
+    lds_barrier();
+  }
+  if (tid == 0) dbase[a.world] = 0;
+  lds_barrier();
+  const int wrw = a.wrw;
+  uint64_t* base = a.arena + tile * (int64_t)a.tile_rows * wrw;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (dest[e] < 0) continue;
+    const int64_t r = row0 + e;
+    const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
+                          ((role_g >> e) & 1u) * ROLE_G;
+    uint64_t* o = base + (int64_t)(dbase[dest[e]] + rank[e]) * wrw;
+    o[0] = (uint64_t)(uint32_t)key[e] | ((uint64_t)role << 32) | ((uint64_t)(uint32_t)sid[e] << 40);
+    o[1] = (uint64_t)(a.seq0 + (r - a.rows.row0));
+    o[2] = (uint64_t)a.rows.ts[r];
+    const bool isa = sid[e] == p.a_stream;
+    const int nrc = isa ? p.nrec_a : p.nrec_b;
+    for (int c = 0; c < nrc; ++c) {
+      const int col = isa ? p.rec_a[c] : p.rec_b[c];
+      o[3 + c] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], r);
+    }
+  }
+}
+
+// Per owner: exclusive prefix of its segment sizes over tiles.
+__global__ __launch_bounds__(512) void k_route_scan(const uint32_t* tcount, int64_t ntiles, int world,
+                                                    uint32_t* toffs, unsigned long long* dcount) {
+  __shared__ uint32_t scratch[16];
+  __shared__ uint32_t carry;
+  const int d = blockIdx.x;
+  if (threadIdx.x == 0) carry = 0;
+  lds_barrier();
+  for (int64_t t0 = 0; t0 < ntiles; t0 += 512) {
+    const int64_t t = t0 + threadIdx.x;
+    const uint32_t c = t < ntiles ? tcount[t * world + d] : 0u;
+    uint32_t total;
+    const uint32_t off = block_excl_scan(c, scratch, &total);
+    if (t < ntiles) toffs[(int64_t)d * ntiles + t] = carry + off;
+    lds_barrier();
+    if (threadIdx.x == 0) carry += total;
+    lds_barrier();
+  }
+  if (threadIdx.x == 0) dcount[d] = carry;
+}
+
+// Copy every tile's owner segments to the owner-contiguous output.
+__global__ __launch_bounds__(256) void k_route_gather(RouteArgs a, int64_t ntiles, const uint32_t* toffs,
+                                                      const unsigned long long* dcount, uint64_t* out) {
+  const int64_t t = blockIdx.x;
+  const int wrw = a.wrw;
+  unsigned long long obase = 0;
+  uint32_t src = 0;
+  for (int d = 0; d < a.world; ++d) {
+    const uint32_t c = a.tcount[t * a.world + d];
+    const uint64_t* s = a.arena + (t * (int64_t)a.tile_rows + src) * wrw;
+    uint64_t* o = out + (int64_t)(obase + toffs[(int64_t)d * ntiles + t]) * wrw;
+    for (int64_t w = threadIdx.x; w < (int64_t)c * wrw; w += blockDim.x) o[w] = s[w];
+    src += c;
+    obase += dcount[d];
+  }
+}
+
+void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
+                  unsigned long long* dcount, uint64_t* out, hipStream_t s) {
+  if (vm) hipLaunchKernelGGL(k_route<true>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+  else hipLaunchKernelGGL(k_route<false>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+  hipLaunchKernelGGL(k_route_scan, dim3((unsigned)a.world), dim3(512), 0, s, a.tcount, ntiles, a.world,
+                     toffs, dcount);
+  hipLaunchKernelGGL(k_route_gather, dim3((unsigned)ntiles), dim3(256), 0, s, a, ntiles, toffs, dcount, out);
 }
 
 // ================================================================ k_walk ==

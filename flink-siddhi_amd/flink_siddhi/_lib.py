@@ -147,7 +147,7 @@ SIGNATURES = {
     "cep_stats": (C.c_int, [C.c_void_p, C.POINTER(cep_stats_t)]),
     "cep_last_error": (C.c_char_p, [C.c_void_p]),
     "cep_record_words": (C.c_int, [C.c_void_p]),
-    "cep_route_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int,
+    "cep_route_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
                                   C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "cep_send_records": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
     "cep_generate": (C.c_int, [C.c_int64, C.c_int64, C.c_uint64, C.c_int64,

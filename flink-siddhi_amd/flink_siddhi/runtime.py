@@ -189,6 +189,50 @@ class SiddhiAppRuntime:
     def flush(self):
         self._check(self._lib.cep_flush(self._h))
 
+    # -- multi-GPU key shuffle (router/HashPartitioner.java:24-26) ---------------
+    def record_words(self) -> int:
+        w = self._lib.cep_record_words(self._h)
+        if w < 0:
+            self._check(-w)
+        return w
+
+    def route(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int,
+              streams=None, out=None):
+        """Sender side of the key shuffle: evaluates the pattern's state
+        filters on a device batch (push-down) and returns (records, counts):
+        a uint64 device tensor [n, record_words] grouped by owner shard
+        (key % world) in arrival order, and the per-owner record counts."""
+        import torch
+        h = self.input_handle(stream_id)
+        defs = self.stream_definition(stream_id)
+        if not _is_device(ts):
+            raise ValueError("route() takes device-resident columns")
+        keep = []
+        ptrs = (C.c_void_p * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            p, k = _ptr(c, np.dtype(L.NUMPY_DTYPES[defs[i][1]]), True)
+            ptrs[i] = p
+            keep.append(k)
+        sp = None
+        if streams is not None:
+            sp, k = _ptr(streams, np.dtype("uint8"), True)
+            keep.append(k)
+        n = _len(ts)
+        w = self.record_words()
+        if out is None or out.shape[0] < n:
+            out = torch.empty((max(n, 1), w), dtype=torch.int64, device=ts.device)
+        b = L.cep_batch(n=n, ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
+                        cols=ptrs, on_device=1)
+        counts = (C.c_int64 * world)()
+        self._check(self._lib.cep_route_batch(self._h, C.byref(b), world, seq0,
+                                              C.c_void_p(out.data_ptr()), out.shape[0], counts))
+        return out, [int(c) for c in counts]
+
+    def send_records(self, recs, n: int, events_represented: int = 0):
+        """Owner side: feed received shuffle records (source-rank order)."""
+        p = C.c_void_p(recs.data_ptr()) if n else None
+        self._check(self._lib.cep_send_records(self._h, p, n, events_represented))
+
     def output_device(self, out_id: str):
         r = L.cep_rows()
         self._check(self._lib.cep_output_device(self._h, out_id.encode(), C.byref(r)))

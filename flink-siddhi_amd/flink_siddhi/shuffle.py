@@ -1,0 +1,57 @@
+"""Key shuffle between GPU shards.
+
+One process per GPU.  Every rank routes its contiguous slice of the global
+event sequence (`SiddhiAppRuntime.route`: push-down filtering + owner =
+key % world, owner-grouped records), exchanges the records with one
+all-to-all (RCCL over xGMI with the "nccl" backend; gloo on CPU), and feeds
+what it received, concatenated in source-rank order (hence in global arrival
+order), to its own engine (`send_records`).  This mirrors Flink's keyBy
+network shuffle in front of the operator (router/HashPartitioner.java:24-26,
+router/DynamicPartitioner.java:43-60).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+def _host_staged() -> bool:
+    # gloo moves host tensors only (CPU tests; rehearsal with ranks sharing a GPU)
+    return dist.get_backend() != "nccl"
+
+
+def exchange_counts(counts: Sequence[int], device) -> List[int]:
+    """All-to-all of the per-owner record counts -> counts received from each source."""
+    world = dist.get_world_size()
+    if _host_staged():
+        device = "cpu"
+    send = torch.tensor(list(counts), dtype=torch.int64, device=device)
+    recv = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_to_all_single(recv, send)
+    return [int(x) for x in recv.tolist()]
+
+
+def exchange(records: torch.Tensor, counts: Sequence[int], out: torch.Tensor = None):
+    """Send records[offsets[d] : offsets[d] + counts[d]] to rank d.
+
+    `records` is [n, words] (int64 words).  Returns (received [m, words],
+    m, per-source counts); received rows are in source-rank order."""
+    words = records.shape[1]
+    recv_counts = exchange_counts(counts, records.device)
+    m = sum(recv_counts)
+    if out is None or out.shape[0] < m:
+        out = torch.empty((max(m, 1), words), dtype=records.dtype, device=records.device)
+    n = sum(counts)
+    osz = [c * words for c in recv_counts]
+    isz = [c * words for c in counts]
+    if _host_staged() and records.is_cuda:
+        host_out = torch.empty(m * words, dtype=records.dtype)
+        dist.all_to_all_single(host_out, records[:n].reshape(-1).cpu(),
+                               output_split_sizes=osz, input_split_sizes=isz)
+        out[:m].view(-1).copy_(host_out)
+    else:
+        dist.all_to_all_single(out[:m].view(-1), records[:n].reshape(-1),
+                               output_split_sizes=osz, input_split_sizes=isz)
+    return out, m, recv_counts

@@ -203,12 +203,17 @@ const char* cep_last_error(cep_app* app);
  * cep_route_batch evaluates the predicates of the app's (single) keyed
  * pattern over a device batch and writes the relevant events as fixed-size
  * records grouped by owner shard (key % world): records for shard r land in
- * rec_out[offsets[r] .. offsets[r]+counts[r]) in arrival order.  The caller
+ * rec_out[offsets[r] .. offsets[r]+counts[r]) in arrival order, offsets being
+ * the exclusive prefix of counts_host.  seq0 = global arrival number of the
+ * batch's first row (rank r of a job sends a contiguous global range).  A
+ * record is cep_record_words(app) 8-byte words: [key | role<<32 | stream<<40,
+ * seq, ts, carried columns...] (device memory, rec_out).  The caller
  * exchanges them (RCCL all-to-all) and feeds the received records, in
  * source-rank order, to the owner's app with cep_send_records. */
 int cep_record_words(cep_app* app);               /* 8-byte words per record */
 int cep_route_batch(cep_app* app, const cep_batch* batch, int world,
-                    void* rec_out, int64_t rec_cap, int64_t* counts_host);
+                    int64_t seq0, void* rec_out, int64_t rec_cap,
+                    int64_t* counts_host);
 int cep_send_records(cep_app* app, const void* recs, int64_t n,
                      int64_t events_represented);
 

@@ -1,0 +1,8 @@
+# Two ranks sharing the box's single GPU (gloo, host-staged exchange): exercises
+# bench.py's multi-GPU shuffle path end to end.  The real N>1 runs use RCCL.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+CEP_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --events 16777216 --steps 2 --warmup 1 \
+  --no-cpu > gpurun_out/multi_rehearsal.log 2>&1
