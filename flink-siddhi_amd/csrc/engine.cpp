@@ -243,12 +243,12 @@ int create_runtime(cep_app* a) {
     hipMemset(o.count, 0, sizeof(unsigned long long));
     a->outs.push_back(std::move(o));
   }
-  const int S = a->opt.pending_slots;
   for (size_t qi = 0; qi < app.queries.size(); ++qi) {
     const Query& q = app.queries[qi];
-    if (q.kind == Q_AGG)
-      return fail(a, CEP_E_UNSUPPORTED, "group-by aggregation is not yet on the device engine");
-    if (q.kind != Q_PATTERN) continue;
+    if (q.kind != Q_PATTERN && q.kind != Q_AGG) continue;
+    const bool agg = q.kind == Q_AGG;
+    // group-by state: one slot of (accumulator, count) pairs per group
+    const int S = agg ? 1 : a->opt.pending_slots;
     PatternRT rt;
     rt.q = (int)qi;
     PatternArgs& p = rt.pa;
@@ -270,18 +270,27 @@ int create_runtime(cep_app* a) {
     p.ncap = (int)q.cap_from_rec.size();
     for (int i = 0; i < p.ncap; ++i) p.cap_from_rec[i] = q.cap_from_rec[i];
     p.rec_words = 2 + std::max(p.nrec_a, p.nrec_b);
-    p.slot_words = 2 + p.ncap;
+    p.slot_words = agg ? 2 * (int)q.aggs.size() : 2 + p.ncap;
     p.key_words = 1 + S * p.slot_words;
     p.pending_slots = S;
     // closed form keeps each record's carried words in LDS (kWalkCapLds)
-    p.closed_form = (q.every && !q.g_in_walk && p.rec_words <= 2 + kWalkCapLds) ? 1 : 0;
+    p.closed_form = (!agg && q.every && !q.g_in_walk && p.rec_words <= 2 + kWalkCapLds) ? 1 : 0;
+    p.agg_mode = agg ? 1 : 0;
+    p.nagg = agg ? (int)q.aggs.size() : 0;
+    for (int i = 0; i < p.nagg; ++i) {
+      p.agg_fn[i] = q.aggs[i].fn;
+      p.agg_arg_type[i] = q.aggs[i].arg_type;
+      p.agg_out_type[i] = q.aggs[i].out_type;
+      p.agg_word[i] = q.aggs[i].word;
+    }
+    p.having_prog = agg ? q.having.off : -1;
     const bool keyed = q.key_col_a >= 0;
     int64_t kcap = keyed ? a->opt.key_capacity : 1;
     p.key_capacity = kcap;
     p.key_stride = keyed ? std::max(1, a->opt.key_stride) : 1;
     p.key_offset = keyed ? a->opt.key_offset : 0;
     if (!keyed && (a->opt.key_stride > 1))
-      return fail(a, CEP_E_UNSUPPORTED, "an unpartitioned pattern cannot be sharded");
+      return fail(a, CEP_E_UNSUPPORTED, "an unpartitioned query cannot be sharded");
     int lg = std::max(0, std::min(12, a->opt.buckets_log2));
     while ((kcap >> lg) > kWalkMaxKeys && lg < 12) ++lg;
     if ((kcap + (1 << lg) - 1) >> lg > kWalkMaxKeys)
@@ -337,7 +346,7 @@ int create_runtime(cep_app* a) {
         pf.n = -1;
       }
     }
-    rt.walk_vm = q.g_in_walk;
+    rt.walk_vm = q.g_in_walk || (agg && q.having.off >= 0);
     for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
     a->pats.push_back(rt);
   }
@@ -492,7 +501,7 @@ int send_device_rows(cep_app* a, const RowsArgs& rows) {
     int rc = CEP_OK;
     if (q.kind == Q_FILTER) {
       rc = run_filter(a, q, rows);
-    } else if (q.kind == Q_PATTERN) {
+    } else if (q.kind == Q_PATTERN || q.kind == Q_AGG) {
       for (auto& rt : a->pats)
         if (rt.q == (int)qi) rc = run_pattern(a, rt, rows);
     }

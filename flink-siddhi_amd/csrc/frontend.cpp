@@ -1,3 +1,4 @@
+#include <algorithm>
 // SiddhiQL subset -> CompiledApp.  See frontend.h.
 //
 // Grammar (the part of Siddhi 4.2.40 that the hot path uses — SURVEY.md §7.1):
@@ -1065,6 +1066,85 @@ int key_column(const StreamSchema& s, const std::string& attr) {
   return i;
 }
 
+// Having over a group-by query: output-attribute references become the
+// select expressions they name (same value, recomputed).
+ExprP inline_outputs(const ExprP& e, const std::vector<SelItem>& sel) {
+  if (e->k == Expr::ATTR && e->out >= 0) return sel[e->out].e;
+  auto c = std::make_shared<Expr>(*e);
+  for (auto& a : c->args) a = inline_outputs(a, sel);
+  return c;
+}
+
+// Copy of program p with every OP_LDCOL column index mapped through `word`.
+Prog remap_cols(CompiledApp* app, const Prog& p, const std::vector<int>& cols) {
+  if (!p.valid()) return p;
+  Prog r = p;
+  r.off = (int)app->code.size();
+  for (int i = 0; i < p.len; ++i) {
+    Ins in = app->code[p.off + i];
+    if (in.op == OP_LDCOL) {
+      int w = -1;
+      for (size_t j = 0; j < cols.size(); ++j)
+        if (cols[j] == (int)in.imm) w = (int)j;
+      in.imm = (uint32_t)w;
+    }
+    app->code.push_back(in);
+  }
+  return r;
+}
+
+void collect_cols(const CompiledApp* app, const Prog& p, std::vector<int>* cols) {
+  if (!p.valid()) return;
+  for (int i = 0; i < p.len; ++i) {
+    const Ins& in = app->code[p.off + i];
+    if (in.op == OP_LDCOL && std::find(cols->begin(), cols->end(), (int)in.imm) == cols->end())
+      cols->push_back((int)in.imm);
+  }
+}
+
+// Device form of a group-by query: the partition pass keeps rows passing the
+// filter as records keyed by the group attribute, carrying every column the
+// select items, aggregate arguments and having read; the walk runs one lane
+// per group over its records in arrival order (running aggregates, having,
+// emission).  Programs are remapped so LDCOL c reads carried word c.
+void lower_aggregation(CompiledApp* app, Query& q) {
+  if ((int)q.aggs.size() > kMaxAggs) fail(CEP_E_UNSUPPORTED, "more than 8 aggregates");
+  std::vector<int> cols;
+  for (auto& a : q.aggs) {
+    if (!a.arg.valid()) continue;
+    const Ins& in = app->code[a.arg.off];
+    if (a.arg.len != 2 || in.op != OP_LDCOL)
+      fail(CEP_E_UNSUPPORTED, "aggregate arguments must be plain attributes on the device");
+    collect_cols(app, a.arg, &cols);
+  }
+  for (auto& it : q.select) collect_cols(app, it.prog, &cols);
+  collect_cols(app, q.having, &cols);
+  if ((int)cols.size() > kMaxCaps) fail(CEP_E_UNSUPPORTED, "group-by query reads too many attributes");
+  q.a_stream = q.in_stream;
+  q.b_stream = -1;
+  q.f = q.filter;
+  q.f_terms = q.filter_terms;
+  q.every = true;
+  q.key_col_a = q.key_col_b = q.key_col;
+  q.rec_cols_a = cols;
+  for (auto& a : q.aggs) {
+    a.word = a.arg.valid() ? (int)(std::find(cols.begin(), cols.end(), (int)app->code[a.arg.off].imm) -
+                                   cols.begin())
+                           : -1;
+    a.arg_type = a.arg.valid() ? app->code[a.arg.off].b : T_LONG;
+  }
+  for (auto& it : q.select) {
+    const Ins& in = app->code[it.prog.off];
+    const bool single = it.prog.len == 2 && in.dst == 0;
+    it.prog = remap_cols(app, it.prog, cols);
+    it.src = SRC_VM;
+    if (single && in.op == OP_LDAGG) it.src = SRC_AGG + (int32_t)in.imm;
+    else if (single && in.op == OP_LDCOL && (int)in.imm == q.key_col) it.src = SRC_KEY;
+    else if (single && in.op == OP_LDCOL) it.src = SRC_REC + (int32_t)app->code[it.prog.off].imm;
+  }
+  q.having = remap_cols(app, q.having, cols);
+}
+
 void compile_single(CompiledApp* app, QueryAst& q) {
   int si = app->input_index(q.stream);
   if (si < 0) fail(CEP_E_UNDEFINED_STREAM, "stream " + q.stream + " is not defined");
@@ -1167,13 +1247,22 @@ void compile_single(CompiledApp* app, QueryAst& q) {
     h.outs = &out.select;
     bind_expr(q.having, h, app);
     if (q.having->t != T_BOOL) fail(CEP_E_PARSE, "having condition must be bool");
-    Loader hl{[](const Expr& e) {
-      if (e.out >= 0) return std::make_pair((uint8_t)OP_LDOUT, (uint32_t)e.out);
-      return std::make_pair((uint8_t)OP_LDCOL, (uint32_t)e.col);
-    }};
-    CodeGen cg(app, hl);
-    out.having = cg.compile(q.having);
+    if (agg) {
+      // output attributes inline as their select expressions, so the device
+      // evaluates having over aggregates and event columns only
+      ExprP hx = inline_outputs(q.having, q.select);
+      CodeGen cg(app, raw);
+      out.having = cg.compile(hx);
+    } else {
+      Loader hl{[](const Expr& e) {
+        if (e.out >= 0) return std::make_pair((uint8_t)OP_LDOUT, (uint32_t)e.out);
+        return std::make_pair((uint8_t)OP_LDCOL, (uint32_t)e.col);
+      }};
+      CodeGen cg(app, hl);
+      out.having = cg.compile(q.having);
+    }
   }
+  if (agg) lower_aggregation(app, out);
   add_output(app, q.out, out.select);
   app->queries.push_back(out);
 }

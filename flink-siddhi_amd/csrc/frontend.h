@@ -33,13 +33,13 @@ struct StreamSchema {
 
 enum QueryKind { Q_FILTER = 0, Q_PATTERN = 1, Q_AGG = 2 };
 
-enum AggFn { AGG_SUM = 0, AGG_COUNT = 1, AGG_AVG = 2, AGG_MIN = 3, AGG_MAX = 4 };
 
 struct AggSpec {
   int fn;
   int arg_type;         // input type (after evaluation of arg program)
   int out_type;
   Prog arg;             // argument program over the current event (unused for count)
+  int word = -1;        // device: carried record word holding the argument (-1: count)
 };
 
 struct OutItem {

@@ -92,6 +92,15 @@ struct PatternArgs {
   int32_t key_stride, key_offset;   // shard ownership (key % stride == offset)
   int32_t buckets_log2;
   int32_t closed_form;     // 1: every && g independent of s1 -> data-parallel walk
+  // group-by / having (agg_mode = 1): per-key running aggregates; state slot 0
+  // holds (accumulator, count) word pairs per aggregate
+  int32_t agg_mode;
+  int32_t nagg;
+  int32_t agg_fn[kMaxAggs];        // AGG_SUM / COUNT / AVG / MIN / MAX
+  int32_t agg_arg_type[kMaxAggs];  // argument column type (record word as load_col)
+  int32_t agg_out_type[kMaxAggs];
+  int32_t agg_word[kMaxAggs];      // carried word of the argument (-1: count())
+  int32_t having_prog;             // -1: none (LDCOL = carried word, LDAGG = running value)
 };
 
 // Fast partition path: every column the pattern reads (key, f / g term

@@ -922,6 +922,10 @@ __device__ __forceinline__ void emit_row(const WalkArgs& a, uint64_t* R, const E
       v = env.cap(src - SRC_CAP);
     } else if (src == SRC_KEY) {
       v = (uint64_t)key;
+    } else if (src >= SRC_AGG && src < SRC_AGG + kMaxAggs) {
+      bool isnull = false;
+      v = env.agg(src - SRC_AGG, &isnull);
+      if (isnull) v = 0;
     } else if (!kVm || (src >= SRC_REC && src < SRC_TS)) {
       v = env.col(src - SRC_REC, 0);
     } else {
@@ -1047,6 +1051,129 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
 #undef SW
 #undef PL
   return matches;
+}
+
+// ---- group-by / having (agg_mode) -----------------------------------------
+// Running aggregates per group in arrival order, following the restatement in
+// oracle/siddhi_oracle.py (_Agg): sum over int/long wraps in 64 bits, sum /
+// avg over float/double accumulate in double, min/max compare in the argument
+// type, count counts; every aggregate of a group sees every kept row.
+struct AggState {
+  uint64_t acc[kMaxAggs];
+  uint64_t cnt[kMaxAggs];
+};
+
+__device__ __forceinline__ double agg_as_double(uint64_t v, int t) {
+  switch (t) {
+    case T_INT: return (double)(int32_t)v;
+    case T_LONG: return (double)(int64_t)v;
+    case T_FLOAT: return (double)as_f32(v);
+    default: return as_f64(v);
+  }
+}
+
+__device__ __forceinline__ bool agg_less(uint64_t a, uint64_t b, int t) {
+  switch (t) {
+    case T_LONG: return (int64_t)a < (int64_t)b;
+    case T_FLOAT: return as_f32(a) < as_f32(b);
+    case T_DOUBLE: return as_f64(a) < as_f64(b);
+    default: return (int32_t)a < (int32_t)b;
+  }
+}
+
+__device__ __forceinline__ void agg_update(const PatternArgs& p, AggState& s, const uint64_t* rec) {
+#pragma unroll
+  for (int j = 0; j < kMaxAggs; ++j) {
+    if (j >= p.nagg) break;
+    const int fn = p.agg_fn[j], at = p.agg_arg_type[j];
+    const uint64_t v = p.agg_word[j] >= 0 ? rec[2 + p.agg_word[j]] : 0;
+    const bool first = s.cnt[j] == 0;
+    s.cnt[j] += 1;
+    if (fn == AGG_SUM) {
+      s.acc[j] = p.agg_out_type[j] == T_LONG ? s.acc[j] + v
+                                             : from_f64(as_f64(s.acc[j]) + agg_as_double(v, at));
+    } else if (fn == AGG_AVG) {
+      s.acc[j] = from_f64(as_f64(s.acc[j]) + agg_as_double(v, at));
+    } else if (fn == AGG_MIN) {
+      if (first || agg_less(v, s.acc[j], at)) s.acc[j] = v;
+    } else if (fn == AGG_MAX) {
+      if (first || agg_less(s.acc[j], v, at)) s.acc[j] = v;
+    }
+  }
+}
+
+struct AggEnv {
+  const PatternArgs* p;
+  const uint64_t* rec;     // current record (carried words at rec[2..])
+  int64_t ev_ts;
+  AggState s;
+  __device__ uint64_t col(int c, int) const { return rec[2 + c]; }
+  __device__ uint64_t cap(int) const { return 0; }
+  __device__ uint64_t outv(int, bool* n) const { *n = true; return 0; }
+  __device__ uint64_t agg(int i, bool* isnull) const {
+    // masked pick (a select chain on i would become a scratch array access)
+    uint64_t acc = 0, cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxAggs; ++j) {
+      const uint64_t m = 0ull - (uint64_t)(i == j);
+      acc |= s.acc[j] & m;
+      cnt |= s.cnt[j] & m;
+    }
+    const int fn = p->agg_fn[i];
+    if (fn == AGG_COUNT) {
+      *isnull = false;
+      return cnt;
+    }
+    *isnull = cnt == 0;
+    if (fn == AGG_AVG) return from_f64(as_f64(acc) / (double)(int64_t)cnt);
+    return acc;
+  }
+  __device__ int64_t ts() const { return ev_ts; }
+};
+
+// One group's records of the window, sequentially (count pass / emit pass).
+template <bool kEmit, bool kVm>
+__device__ uint32_t agg_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int k, int bucket, int kpb,
+                            int64_t ts_base, int64_t seq_base, unsigned long long out_pos) {
+  const PatternArgs& p = a.pat;
+  const int64_t idx = (int64_t)bucket * kpb + k;
+  const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
+  const int64_t ks = a.kstride;
+  const int rw = p.rec_words;
+  AggEnv env{&p, nullptr, 0, {}};
+  const bool live = (L.khdr[k] & 0xffu) != 0;
+#pragma unroll
+  for (int j = 0; j < kMaxAggs; ++j) {
+    env.s.acc[j] = (live && j < p.nagg) ? a.kslot[(int64_t)(2 * j) * ks + idx] : 0;
+    env.s.cnt[j] = (live && j < p.nagg) ? a.kslot[(int64_t)(2 * j + 1) * ks + idx] : 0;
+  }
+  uint32_t emitted = 0;
+  for (uint32_t q = L.kstart[k]; q < L.kstart[k + 1]; ++q) {
+    const uint64_t* rec = a.recs + (int64_t)L.wrec[L.sorted[q]] * rw;
+    agg_update(p, env.s, rec);
+    env.rec = rec;
+    env.ev_ts = rec_ts(rec, ts_base);
+    bool pass = true;
+    if (kVm && p.having_prog >= 0) {
+      bool isnull = false;
+      const uint64_t v = eval_env(a.vm, p.having_prog, R, env, &isnull);
+      pass = !isnull && (v & 1u);
+    }
+    if (!pass) continue;
+    if (kEmit) emit_row<kVm>(a, R, env, key_value(p, kl), rec_seq(rec, seq_base), out_pos + emitted);
+    ++emitted;
+  }
+  if (kEmit) {
+#pragma unroll
+    for (int j = 0; j < kMaxAggs; ++j) {
+      if (j >= p.nagg) break;
+      a.kslot[(int64_t)(2 * j) * ks + idx] = env.s.acc[j];
+      a.kslot[(int64_t)(2 * j + 1) * ks + idx] = env.s.cnt[j];
+    }
+    L.khdr[k] = 1u;
+    a.khdr[idx] = 1u;
+  }
+  return emitted;
 }
 
 // XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
@@ -1201,7 +1328,21 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     lds_barrier();
     WALK_STAMP(3);
 
-    if (p.closed_form) {
+    if (p.agg_mode) {
+      // ---- group-by / having: one lane per group, count pass + emit pass ----
+      uint32_t mine = 0;
+      for (int k = tid; k < kpb; k += kWalkThreads)
+        if (L.kstart[k + 1] > L.kstart[k])
+          mine += agg_key<false, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, 0);
+      uint32_t total;
+      const uint32_t off = block_excl_scan(mine, L.scratch, &total);
+      if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
+      lds_barrier();
+      unsigned long long pos = L.base + off;
+      for (int k = tid; k < kpb; k += kWalkThreads)
+        if (L.kstart[k + 1] > L.kstart[k])
+          pos += agg_key<true, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, pos);
+    } else if (p.closed_form) {
       // ---- closed form: A matches the next B of its key within W -----------
       const int S = p.pending_slots, sw = p.slot_words;
       // stage the carried state slots of every touched key in LDS: all global

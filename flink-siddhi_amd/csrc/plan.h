@@ -91,7 +91,11 @@ enum : int32_t {
   SRC_REC = 64,     // + i: record word i of the completing event (pattern)
   SRC_TS = 128,     // event timestamp of the completing / current event
   SRC_KEY = 129,    // the partition key (pattern under `partition with`)
+  SRC_AGG = 160,    // + i: running value of aggregate i (group-by query)
 };
+
+constexpr int kMaxAggs = 8;
+enum AggFn { AGG_SUM = 0, AGG_COUNT = 1, AGG_AVG = 2, AGG_MIN = 3, AGG_MAX = 4 };
 
 // Role bits carried in partition records (pattern path).
 enum : uint32_t {
