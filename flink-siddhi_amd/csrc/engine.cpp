@@ -284,6 +284,40 @@ int create_runtime(cep_app* a) {
       p.agg_word[i] = q.aggs[i].word;
     }
     p.having_prog = agg ? q.having.off : -1;
+    if (q.nfa) {
+      if (app.inputs.size() > 8)
+        return fail(a, CEP_E_UNSUPPORTED, "patterns / sequences over apps with more than 8 input streams");
+      p.nfa_mode = 1;
+      p.nfa_seq = q.sequence ? 1 : 0;
+      p.nstates = (int)q.nstates.size();
+      p.closed_form = 0;
+      p.ncap = (int)q.ncaps.size();
+      p.slot_words = 2 + p.ncap;
+      p.key_words = 1 + S * p.slot_words;
+      p.stream_mask = 0;
+      for (int j = 0; j < p.nstates; ++j) {
+        const auto& st = q.nstates[j];
+        p.st_stream[j] = st.stream;
+        p.st_min[j] = st.min_count;
+        p.st_max[j] = st.max_count;
+        p.st_raw[j] = st.raw.off;
+        p.st_walk[j] = st.walk.off;
+        p.stream_mask |= 1 << st.stream;
+      }
+      for (int j = 0; j < p.nstates; ++j) {
+        bool opt = true;
+        for (int k = j + 1; k < p.nstates; ++k) opt = opt && q.nstates[k].min_count == 0;
+        p.st_tail_opt[j] = opt ? 1 : 0;
+      }
+      for (int i = 0; i < 8; ++i) p.key_col_s[i] = i < (int)q.key_col_s.size() ? q.key_col_s[i] : -1;
+      for (int i = 0; i < p.ncap; ++i) {
+        p.cap_state[i] = q.ncaps[i].state;
+        p.cap_index[i] = q.ncaps[i].index;
+        p.cap_word[i] = q.ncaps[i].word;
+      }
+    }
+    // NFA patterns stage advanced partials in a second bank of S slots
+    const int bank = q.nfa ? 2 : 1;
     const bool keyed = q.key_col_a >= 0;
     int64_t kcap = keyed ? a->opt.key_capacity : 1;
     p.key_capacity = kcap;
@@ -301,7 +335,7 @@ int create_runtime(cep_app* a) {
     const int64_t kpb = (kc + (1 << lg) - 1) >> lg;
     rt.kstride = kpb << lg;
     if (!dev_ensure(&rt.khdr, (size_t)rt.kstride * 4, a->stream, false) ||
-        !dev_ensure(&rt.kslot, (size_t)rt.kstride * S * p.slot_words * 8, a->stream, false) ||
+        !dev_ensure(&rt.kslot, (size_t)rt.kstride * bank * S * p.slot_words * 8, a->stream, false) ||
         !dev_ensure(&rt.chunk_base[0], 64, a->stream, false) ||
         !dev_ensure(&rt.chunk_base[1], 64, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (pattern state)");
@@ -321,7 +355,7 @@ int create_runtime(cep_app* a) {
         return fail(a, CEP_E_DEVICE, "hipEventCreate failed");
     }
     rt.extra_bound = (int64_t)S * kc;
-    rt.part_vm = (q.f.off >= 0 && q.f_terms.n < 0) || (q.g_raw.off >= 0 && q.g_terms.n < 0);
+    rt.part_vm = (q.f.off >= 0 && q.f_terms.n < 0) || (q.g_raw.off >= 0 && q.g_terms.n < 0) || q.nfa;
     // fast partition path: all columns the pass reads fit kPref registers
     if (!rt.part_vm && q.key_col_a == q.key_col_b && p.nrec_a <= kPfRec && p.nrec_b <= kPfRec) {
       PrefPlan& pf = rt.pref;
@@ -346,7 +380,8 @@ int create_runtime(cep_app* a) {
         pf.n = -1;
       }
     }
-    rt.walk_vm = q.g_in_walk || (agg && q.having.off >= 0);
+    // group-by and N-state / sequence walks live in the VM build of k_walk
+    rt.walk_vm = q.g_in_walk || agg || q.nfa;
     for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
     a->pats.push_back(rt);
   }

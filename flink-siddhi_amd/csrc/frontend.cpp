@@ -1275,11 +1275,139 @@ int index_of(std::vector<int>& v, int x, bool add) {
   return (int)v.size() - 1;
 }
 
+// N-state patterns and sequences (with count states in sequences): one NFA
+// lane per key in the walk.  Semantics follow oracle/siddhi_oracle.py
+// (_pattern_event / _sequence_event).
+void compile_nfa(CompiledApp* app, QueryAst& q) {
+  const int n = (int)q.states.size();
+  if (n < 1 || n > kMaxStates) fail(CEP_E_UNSUPPORTED, "patterns / sequences of more than 6 states");
+  for (int j = 0; j < n; ++j) {
+    auto& st = q.states[j];
+    if (app->input_index(st.stream) < 0)
+      fail(CEP_E_UNDEFINED_STREAM, "stream " + st.stream + " is not defined");
+    if (j > 0 && st.every) fail(CEP_E_UNSUPPORTED, "'every' on a non-start state");
+    if (!q.sequence && (st.min_count != 1 || st.max_count != 1))
+      fail(CEP_E_UNSUPPORTED, "count states in patterns are not supported");
+    for (int k = 0; k < j; ++k)
+      if (q.states[k].alias == st.alias && !st.alias.empty()) fail(CEP_E_PARSE, "duplicate state alias");
+  }
+  if (!q.group_by.empty() || q.having) fail(CEP_E_UNSUPPORTED, "group by / having on patterns");
+  if (q.select_all) fail(CEP_E_PARSE, "pattern query needs an explicit select");
+  Query out;
+  out.kind = Q_PATTERN;
+  out.nfa = true;
+  out.sequence = q.sequence;
+  out.out_stream = q.out;
+  out.every = q.states[0].every;
+  out.within = q.within;
+  out.a_stream = app->input_index(q.states[0].stream);
+  Ctx c;
+  c.mode = Ctx::PATTERN;
+  for (auto& st : q.states) {
+    c.states.push_back(&app->inputs[app->input_index(st.stream)]);
+    c.aliases.push_back(st.alias);
+  }
+  // bind conditions and select
+  for (int j = 0; j < n; ++j) {
+    if (!q.states[j].cond) continue;
+    c.cur_state = j;
+    bind_expr(q.states[j].cond, c, app);
+    if (q.states[j].cond->t != T_BOOL) fail(CEP_E_PARSE, "condition must be bool");
+  }
+  c.cur_state = -1;
+  std::set<std::string> names;
+  for (auto& it : q.select) {
+    if (has_call(it.e)) fail(CEP_E_UNSUPPORTED, "aggregates in pattern select");
+    bind_expr(it.e, c, app);
+    if (it.e->t == T_OBJECT) fail(CEP_E_UNSUPPORTED, "object attributes in select");
+    if (!names.insert(it.name).second) fail(CEP_E_PARSE, "duplicate output attribute " + it.name);
+  }
+  // partition keys per input stream
+  out.key_col_s.assign(app->inputs.size(), -1);
+  if (q.partitioned) {
+    for (auto& st : q.states) {
+      auto it = q.partition.find(st.stream);
+      if (it == q.partition.end())
+        fail(CEP_E_PARSE, "pattern stream not covered by the enclosing partition");
+      const int si = app->input_index(st.stream);
+      out.key_col_s[si] = key_column(app->inputs[si], it->second);
+    }
+  }
+  out.key_col_a = out.key_col_b = q.partitioned ? out.key_col_s[out.a_stream] : -1;
+  // records carry one column list for every stream (batches mixing streams
+  // require identical definitions)
+  auto rec_word = [&](int col) { return index_of(out.rec_cols_a, col, true); };
+  // captures: (state, index, column); "cur" (-1) in a select means the first event
+  auto cap_of = [&](int state, int idx, int col) {
+    const int index = idx == -2 ? -1 : (idx < 0 ? 0 : idx);
+    const int w = rec_word(col);
+    for (size_t i = 0; i < out.ncaps.size(); ++i)
+      if (out.ncaps[i].state == state && out.ncaps[i].index == index && out.ncaps[i].word == w)
+        return (int)i;
+    out.ncaps.push_back({state, index, w});
+    return (int)out.ncaps.size() - 1;
+  };
+  auto key_ref = [&](const ExprP& e) {
+    return q.partitioned && e->k == Expr::ATTR && e->state >= 0 &&
+           e->col == out.key_col_s[app->input_index(q.states[e->state].stream)];
+  };
+  std::function<bool(const ExprP&, int)> self_only = [&](const ExprP& e, int j) -> bool {
+    if (e->k == Expr::ATTR && (e->state != j || e->idx != -1)) return false;
+    for (auto& a : e->args)
+      if (!self_only(a, j)) return false;
+    return true;
+  };
+  Loader raw{[](const Expr& e) { return std::make_pair((uint8_t)OP_LDCOL, (uint32_t)e.col); }};
+  for (int j = 0; j < n; ++j) {
+    Query::NState ns;
+    ns.stream = app->input_index(q.states[j].stream);
+    ns.min_count = q.states[j].min_count;
+    ns.max_count = q.states[j].max_count;
+    if (q.states[j].cond) {
+      if (self_only(q.states[j].cond, j)) {
+        CodeGen cg(app, raw);
+        ns.raw = cg.compile(q.states[j].cond);
+      } else {
+        const int jj = j;
+        Loader wl{[&, jj](const Expr& e) {
+          if (e.state == jj && e.idx == -1)
+            return std::make_pair((uint8_t)OP_LDCOL, (uint32_t)rec_word(e.col));
+          return std::make_pair((uint8_t)OP_LDCAP, (uint32_t)cap_of(e.state, e.idx, e.col));
+        }};
+        CodeGen cg(app, wl);
+        ns.walk = cg.compile(q.states[j].cond);
+      }
+    }
+    out.nstates.push_back(ns);
+  }
+  Loader sl{[&](const Expr& e) {
+    return std::make_pair((uint8_t)OP_LDCAP, (uint32_t)cap_of(e.state, e.idx, e.col));
+  }};
+  for (auto& it : q.select) {
+    OutItem oi;
+    oi.name = it.name;
+    oi.type = it.e->t;
+    if (key_ref(it.e)) {
+      oi.prog = Prog{};
+      oi.src = SRC_KEY;
+    } else {
+      CodeGen cg(app, sl);
+      oi.prog = cg.compile(it.e);
+      oi.src = direct_source(app, oi.prog);   // SRC_CAP + i
+    }
+    out.select.push_back(oi);
+  }
+  if ((int)out.ncaps.size() > kMaxCaps || (int)out.rec_cols_a.size() > kMaxCaps)
+    fail(CEP_E_UNSUPPORTED, "too many captured attributes");
+  out.rec_cols_b = out.rec_cols_a;
+  add_output(app, q.out, out.select);
+  app->queries.push_back(out);
+}
+
 void compile_pattern(CompiledApp* app, QueryAst& q) {
-  if (q.sequence)
-    fail(CEP_E_UNSUPPORTED, "sequences (',') are not yet supported by the device engine");
-  if (q.states.size() != 2)
-    fail(CEP_E_UNSUPPORTED, "only 2-state patterns are supported by the device engine");
+  bool counts = false;
+  for (auto& s : q.states) counts |= s.min_count != 1 || s.max_count != 1;
+  if (q.sequence || q.states.size() != 2 || counts) return compile_nfa(app, q);
   for (auto& s : q.states) {
     if (app->input_index(s.stream) < 0)
       fail(CEP_E_UNDEFINED_STREAM, "stream " + s.stream + " is not defined");

@@ -77,6 +77,24 @@ struct Query {
   std::vector<int> rec_cols_a;   // raw columns carried in A-stream records
   std::vector<int> rec_cols_b;   // raw columns carried in B-stream records
   std::vector<int> cap_from_rec; // pending capture word i <- A-record word cap_from_rec[i]
+
+  // ---- N-state pattern / sequence (general NFA walk): `nfa` queries keep
+  // every event of the states' streams (sequences) or every event some
+  // state's own condition accepts (patterns) as records carrying rec_cols_a
+  struct NState {
+    int stream = -1;
+    int min_count = 1, max_count = 1;   // max -1: unbounded
+    Prog raw;      // condition over the event's own columns (partition pass)
+    Prog walk;     // condition reading earlier states (walk: LDCOL word, LDCAP capture)
+  };
+  struct NCap {
+    int state, index, word;           // index: k-th event of the state (0 = first), -1 = last
+  };
+  bool nfa = false;
+  bool sequence = false;
+  std::vector<NState> nstates;
+  std::vector<NCap> ncaps;
+  std::vector<int> key_col_s;    // per input stream handle: partition key column (-1)
 };
 
 struct CompiledApp {

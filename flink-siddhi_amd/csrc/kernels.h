@@ -101,6 +101,19 @@ struct PatternArgs {
   int32_t agg_out_type[kMaxAggs];
   int32_t agg_word[kMaxAggs];      // carried word of the argument (-1: count())
   int32_t having_prog;             // -1: none (LDCOL = carried word, LDAGG = running value)
+  // N-state pattern / sequence (nfa_mode = 1): one NFA lane per key; a
+  // partial is a state slot {start ts, state | count << 8, captures...}
+  int32_t nfa_mode;
+  int32_t nfa_seq;                 // 1: sequence (strict contiguity, count states)
+  int32_t nstates;
+  int32_t stream_mask;             // input handles the query reads
+  int32_t st_stream[kMaxStates];
+  int32_t st_min[kMaxStates], st_max[kMaxStates];   // max -1: unbounded
+  int32_t st_raw[kMaxStates];      // own-column condition (partition pass), -1: none
+  int32_t st_walk[kMaxStates];     // condition reading captures (walk VM), -1: none
+  int32_t st_tail_opt[kMaxStates]; // every state after j is optional (min 0)
+  int32_t key_col_s[8];            // partition key column per input handle
+  int32_t cap_state[kMaxCaps], cap_index[kMaxCaps], cap_word[kMaxCaps];
 };
 
 // Fast partition path: every column the pattern reads (key, f / g term

@@ -406,6 +406,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
   int64_t key[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) key[e] = 0;
+  uint32_t nrole[kVm ? E : 1];   // N-state pattern / sequence roles (VM path)
   // fast path: the lane's rows stay in registers for the record build
   uint64_t tsv[kPf ? E : 1];
   uint64_t pv[kPf ? kPref : 1][kPf ? E : 1];
@@ -516,29 +517,55 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
         }
         if (bad) set_err(a.err, ERR_ORDER);
       }
-      if (is_a) role_a = is_a & eval_run<E, kVm>(p.f_terms, a.vm, p.f_prog, R, a.rows, row0, nvalid);
-      if (is_b) {
-        if (p.g_walk_prog >= 0) {
-          role_b = is_b;
-        } else {
-          role_b = is_b & eval_run<E, kVm>(p.g_terms, a.vm, p.g_raw_prog, R, a.rows, row0, nvalid);
-          role_g = role_b;
+      bool nfa = false;
+      if constexpr (kVm) nfa = p.nfa_mode != 0;
+      if (nfa) {
+        // N-state pattern / sequence: role bit j = state j's own condition
+        // accepts the row (or it is checked in the walk); bit 7 = row kept.
+        // Sequences keep every row of their streams (strict contiguity).
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          key[e] = 0;
+          if constexpr (kVm) {
+            nrole[e] = 0;
+            if (e >= nvalid || sid[e] < 0 || !((p.stream_mask >> sid[e]) & 1)) continue;
+            uint32_t r = 0x80u;
+            for (int j = 0; j < p.nstates; ++j) {
+              if (p.st_stream[j] != sid[e]) continue;
+              if (p.st_raw[j] < 0 || eval_pred(a.vm, p.st_raw[j], R, RowEnv{&a.rows, row0 + e}))
+                r |= 1u << j;
+            }
+            if (!p.nfa_seq && r == 0x80u) continue;   // patterns: no state can use it
+            nrole[e] = r;
+            const int kc = p.key_col_s[sid[e]];
+            if (kc >= 0) key[e] = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e);
+          }
         }
-      }
+      } else {
+        if (is_a) role_a = is_a & eval_run<E, kVm>(p.f_terms, a.vm, p.f_prog, R, a.rows, row0, nvalid);
+        if (is_b) {
+          if (p.g_walk_prog >= 0) {
+            role_b = is_b;
+          } else {
+            role_b = is_b & eval_run<E, kVm>(p.g_terms, a.vm, p.g_raw_prog, R, a.rows, row0, nvalid);
+            role_g = role_b;
+          }
+        }
 #pragma unroll
-      for (int e = 0; e < E; ++e) key[e] = 0;
-      if (role_a | role_b) {
-        if (p.key_col_a >= 0 && p.key_col_a == p.key_col_b) {
-          uint64_t k[E];
-          load_run<E>(a.rows.cols.p[p.key_col_a], a.rows.cols.t[p.key_col_a], row0, nvalid, k);
+        for (int e = 0; e < E; ++e) key[e] = 0;
+        if (role_a | role_b) {
+          if (p.key_col_a >= 0 && p.key_col_a == p.key_col_b) {
+            uint64_t k[E];
+            load_run<E>(a.rows.cols.p[p.key_col_a], a.rows.cols.t[p.key_col_a], row0, nvalid, k);
 #pragma unroll
-          for (int e = 0; e < E; ++e) key[e] = (int64_t)k[e];
-        } else {
+            for (int e = 0; e < E; ++e) key[e] = (int64_t)k[e];
+          } else {
 #pragma unroll
-          for (int e = 0; e < E; ++e) {
-            if (((role_a | role_b) >> e) & 1u) {
-              const int kc = sid[e] == p.a_stream ? p.key_col_a : p.key_col_b;
-              if (kc >= 0) key[e] = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e);
+            for (int e = 0; e < E; ++e) {
+              if (((role_a | role_b) >> e) & 1u) {
+                const int kc = sid[e] == p.a_stream ? p.key_col_a : p.key_col_b;
+                if (kc >= 0) key[e] = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e);
+              }
             }
           }
         }
@@ -546,8 +573,11 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
-                            ((role_g >> e) & 1u) * ROLE_G;
+      uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
+                      ((role_g >> e) & 1u) * ROLE_G;
+      if constexpr (kVm) {
+        if (p.nfa_mode) role = nrole[e];
+      }
       if (!role) continue;
       if (key[e] < 0 || (key[e] % p.key_stride) != p.key_offset) {
         set_err(a.err, ERR_KEY_RANGE);
@@ -558,8 +588,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       const int bucket = (int)(kfield & (P - 1));
       key[e] = kfield;
       const uint32_t rank = atomicAdd(&hist[bucket], 1u);
-      // bits 0-10 rank in tile, 11-13 role, 14-25 bucket
-      packed[e] = ((uint32_t)bucket << 14) | (role << 11) | rank;
+      // bits 0-10 rank in tile, 11-22 bucket, 23-30 role (never all ones)
+      packed[e] = (role << 23) | ((uint32_t)bucket << 11) | rank;
     }
   }
   lds_barrier();
@@ -596,8 +626,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       if (packed[e] == 0xffffffffu) continue;
-      const uint32_t b = packed[e] >> 14, rank = packed[e] & 0x7ffu;
-      const uint32_t role = (packed[e] >> 11) & 7u;
+      const uint32_t b = (packed[e] >> 11) & 0xfffu, rank = packed[e] & 0x7ffu;
+      const uint32_t role = (packed[e] >> 23) & 0xffu;
       const uint32_t slot = hist[b] + rank;
       // explicit address spaces (a generic pointer would make these flat stores)
       const int64_t so = (int64_t)slot * rw;
@@ -1176,6 +1206,169 @@ __device__ uint32_t agg_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int k, i
   return emitted;
 }
 
+// ---- N-state patterns / sequences (nfa_mode) --------------------------------
+// One lane walks one key's records in arrival order over the key's partial
+// matches, kept in its state slots {start ts, state | count << 8, captures}.
+// Restates oracle/siddhi_oracle.py _pattern_event / _sequence_event (SURVEY
+// App. A.3-A.5).  Patterns: a partial advances when the event is on its next
+// state's stream and the condition holds (else it stays), expired partials
+// are dropped, advanced partials move behind the ones that stayed, a start
+// event appends a new partial.  Sequences: every event of the query's streams
+// either advances a partial (staying in a count state, or moving to a later
+// state skipping optional ones) or discards it.  Matches reserve output rows
+// one by one (a lane's rows of one event stay in creation order).
+template <bool kVm>
+__device__ __forceinline__ bool nfa_cond(const WalkArgs& a, uint64_t* R, int j, uint32_t role,
+                                         const uint64_t* slot, const uint64_t* rec, int64_t ts_base) {
+  const PatternArgs& p = a.pat;
+  if (!((role >> j) & 1u)) return false;
+  if (!kVm || p.st_walk[j] < 0) return true;
+  const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, a.kstride};
+  bool isnull = false;
+  const uint64_t v = eval_env(a.vm, p.st_walk[j], R, env, &isnull);
+  return !isnull && (v & 1u);
+}
+
+// Collect the event into state j of the partial at `slot` (count c after it).
+__device__ __forceinline__ void nfa_collect(const PatternArgs& p, uint64_t* slot, int64_t ks, int j,
+                                            int c, const uint64_t* rec) {
+  slot[ks] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)c << 8);
+  for (int i = 0; i < p.ncap; ++i) {
+    if (p.cap_state[i] != j) continue;
+    if (p.cap_index[i] < 0 || p.cap_index[i] + 1 == c) slot[(2 + i) * ks] = rec[2 + p.cap_word[i]];
+  }
+}
+
+template <bool kVm>
+__device__ __forceinline__ void nfa_emit(const WalkArgs& a, uint64_t* R, const uint64_t* slot,
+                                         const uint64_t* rec, int64_t ts_base, int64_t seq_base,
+                                         int64_t kl) {
+  const PatternArgs& p = a.pat;
+  const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, a.kstride};
+  const unsigned long long pos = atomicAdd(a.out.count, 1ull);
+  emit_row<kVm>(a, R, env, key_value(p, kl), rec_seq(rec, seq_base), pos);
+}
+
+template <bool kVm>
+__device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int k, int bucket, int kpb,
+                        int64_t ts_base, int64_t seq_base) {
+  const PatternArgs& p = a.pat;
+  const int S = p.pending_slots, sw = p.slot_words, rw = p.rec_words, N = p.nstates;
+  const int64_t ks = a.kstride;
+  const int64_t idx = (int64_t)bucket * kpb + k;
+  const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
+  uint64_t* sl = a.kslot + idx;
+#define NSLOT(j) (sl + (int64_t)(j) * sw * ks)
+  auto copy_slot = [&](int dst, int src) {
+    if (dst == src) return;
+    for (int x = 0; x < sw; ++x) NSLOT(dst)[x * ks] = NSLOT(src)[x * ks];
+  };
+  auto settle = [&](uint64_t* slot, int j, int c, const uint64_t* rec) -> bool {
+    // returns whether the partial survives; emits when complete
+    const bool done = c >= p.st_min[j] && p.st_tail_opt[j];
+    if (!done) return true;
+    nfa_emit<kVm>(a, R, slot, rec, ts_base, seq_base, kl);
+    return j == N - 1 && (p.st_max[j] < 0 || c < p.st_max[j]);
+  };
+  uint32_t hdr = L.khdr[k];
+  int n = (int)(hdr & 0xffu);
+  bool started = ((hdr >> 8) & 1u) != 0;
+  for (uint32_t q = L.kstart[k]; q < L.kstart[k + 1]; ++q) {
+    const uint64_t* rec = a.recs + (int64_t)L.wrec[L.sorted[q]] * rw;
+    const uint64_t h = rec[0];
+    const uint32_t role = (uint32_t)(h >> 32) & 0xffu;
+    const int stream = (int)((h >> 40) & 0xffu);
+    const int64_t ts = rec_ts(rec, ts_base);
+    int m = 0;
+    if (!p.nfa_seq) {
+      int nf = 0;   // advanced partials, staged in slots [S, 2S)
+      for (int i = 0; i < n; ++i) {
+        uint64_t* si = NSLOT(i);
+        const int j = (int)(si[ks] & 0xffu);
+        if (p.st_stream[j] != stream) { copy_slot(m++, i); continue; }
+        if (p.within >= 0) {
+          const int64_t d = ts - (int64_t)si[0];
+          if ((d < 0 ? -d : d) > p.within) continue;   // expired: dropped
+        }
+        if (!nfa_cond<kVm>(a, R, j, role, si, rec, ts_base)) { copy_slot(m++, i); continue; }
+        if (j + 1 == N) {
+          nfa_collect(p, si, ks, j, 1, rec);
+          nfa_emit<kVm>(a, R, si, rec, ts_base, seq_base, kl);   // consumed
+          continue;
+        }
+        copy_slot(S + nf, i);
+        nfa_collect(p, NSLOT(S + nf), ks, j + 1 - 1, 1, rec);
+        NSLOT(S + nf)[ks] = (uint64_t)(j + 1);
+        ++nf;
+      }
+      if (p.st_stream[0] == stream && (p.every || !started) &&
+          nfa_cond<kVm>(a, R, 0, role, nullptr, rec, ts_base)) {
+        started = true;
+        uint64_t* ns = NSLOT(S + nf);
+        ns[0] = (uint64_t)ts;
+        for (int x = 2; x < sw; ++x) ns[x * ks] = 0;
+        nfa_collect(p, ns, ks, 0, 1, rec);
+        if (N == 1) {
+          nfa_emit<kVm>(a, R, ns, rec, ts_base, seq_base, kl);
+        } else {
+          ns[ks] = 1;
+          ++nf;
+        }
+      }
+      if (m + nf > S) {
+        set_err(a.err, ERR_PENDING);
+        nf = S - m;
+      }
+      for (int f = 0; f < nf; ++f) copy_slot(m + f, S + f);
+      n = m + nf;
+    } else {
+      for (int i = 0; i < n; ++i) {
+        uint64_t* si = NSLOT(i);
+        if (p.within >= 0) {
+          const int64_t d = ts - (int64_t)si[0];
+          if ((d < 0 ? -d : d) > p.within) continue;
+        }
+        const uint64_t jc = si[ks];
+        const int j = (int)(jc & 0xffu), c = (int)(jc >> 8);
+        bool keep = false;
+        if (p.st_stream[j] == stream && (p.st_max[j] < 0 || c < p.st_max[j]) &&
+            nfa_cond<kVm>(a, R, j, role, si, rec, ts_base)) {
+          nfa_collect(p, si, ks, j, c + 1, rec);              // stay in the count state
+          keep = settle(si, j, c + 1, rec);
+        } else if (c >= p.st_min[j]) {
+          for (int j2 = j + 1; j2 < N; ++j2) {                // move on, skipping optional states
+            if (p.st_stream[j2] == stream && nfa_cond<kVm>(a, R, j2, role, si, rec, ts_base)) {
+              nfa_collect(p, si, ks, j2, 1, rec);
+              keep = settle(si, j2, 1, rec);
+              break;
+            }
+            if (p.st_min[j2] > 0) break;
+          }
+        }
+        if (keep) copy_slot(m++, i);                          // else discarded (contiguity)
+      }
+      if (p.st_stream[0] == stream && (p.every || !started) &&
+          nfa_cond<kVm>(a, R, 0, role, nullptr, rec, ts_base)) {
+        started = true;
+        if (m >= S) {
+          set_err(a.err, ERR_PENDING);
+        } else {
+          uint64_t* ns = NSLOT(m);
+          ns[0] = (uint64_t)ts;
+          for (int x = 2; x < sw; ++x) ns[x * ks] = 0;
+          nfa_collect(p, ns, ks, 0, 1, rec);
+          if (settle(ns, 0, 1, rec)) ++m;
+        }
+      }
+      n = m;
+    }
+  }
+#undef NSLOT
+  const uint32_t nh = (uint32_t)n | ((started ? 1u : 0u) << 8);
+  L.khdr[k] = nh;
+  a.khdr[idx] = nh;
+}
+
 // XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
 // §Workgroup dispatch), so consecutive buckets — which share tile-offset
 // cache lines — are given to blocks of one XCD.  Speed only, never correctness.
@@ -1328,20 +1521,31 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     lds_barrier();
     WALK_STAMP(3);
 
-    if (p.agg_mode) {
+    bool nfa = false;
+    if constexpr (kVm) nfa = p.nfa_mode != 0;   // (the NFA walk needs the VM build)
+    if (nfa) {
+      // ---- N-state pattern / sequence: one NFA lane per key -----------------
+      if constexpr (kVm) {
+        for (int k = tid; k < kpb; k += kWalkThreads)
+          if (L.kstart[k + 1] > L.kstart[k]) nfa_key<kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base);
+      }
+    } else if (kVm && p.agg_mode) {
       // ---- group-by / having: one lane per group, count pass + emit pass ----
+      // (VM build only: keeps the pattern fast path lean)
       uint32_t mine = 0;
-      for (int k = tid; k < kpb; k += kWalkThreads)
-        if (L.kstart[k + 1] > L.kstart[k])
-          mine += agg_key<false, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, 0);
+      if constexpr (kVm)
+        for (int k = tid; k < kpb; k += kWalkThreads)
+          if (L.kstart[k + 1] > L.kstart[k])
+            mine += agg_key<false, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, 0);
       uint32_t total;
       const uint32_t off = block_excl_scan(mine, L.scratch, &total);
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
       lds_barrier();
       unsigned long long pos = L.base + off;
-      for (int k = tid; k < kpb; k += kWalkThreads)
-        if (L.kstart[k + 1] > L.kstart[k])
-          pos += agg_key<true, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, pos);
+      if constexpr (kVm)
+        for (int k = tid; k < kpb; k += kWalkThreads)
+          if (L.kstart[k + 1] > L.kstart[k])
+            pos += agg_key<true, kVm>(a, L, R, k, bucket, kpb, ts_base, seq_base, pos);
     } else if (p.closed_form) {
       // ---- closed form: A matches the next B of its key within W -----------
       const int S = p.pending_slots, sw = p.slot_words;

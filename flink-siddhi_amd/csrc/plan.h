@@ -95,6 +95,7 @@ enum : int32_t {
 };
 
 constexpr int kMaxAggs = 8;
+constexpr int kMaxStates = 6;     // states of an N-state pattern / sequence
 enum AggFn { AGG_SUM = 0, AGG_COUNT = 1, AGG_AVG = 2, AGG_MIN = 3, AGG_MAX = 4 };
 
 // Role bits carried in partition records (pattern path).

@@ -1,0 +1,94 @@
+"""N-state patterns and sequences with count states on the device (SURVEY.md
+§8 row a3: `every s1=A, s2=B+, s3=C within` and friends) vs the CPU oracle,
+bit-exact, on seeded three-stream workloads."""
+import numpy as np
+import pytest
+
+import flink_siddhi as fs
+from flink_siddhi import workload
+from helpers import assert_same_rows, engine_rows, oracle_run
+
+pytestmark = pytest.mark.gpu
+
+EV3 = ("define stream A (k int, ts long, id int, price double);"
+       "define stream B (k int, ts long, id int, price double);"
+       "define stream C (k int, ts long, id int, price double);")
+NAMES = ("A", "B", "C")
+
+
+def three_streams(n, keys, seed_shift=0):
+    w = workload.generate(seed_shift, n, keys, rate=1)
+    w["stream"] = ((w["price"] * 1000).astype(np.int64) % 3).astype(np.uint8)
+    return w
+
+
+def events(w):
+    k, ts, i, p, st = (w[c].tolist() for c in ("k", "ts", "id", "price", "stream"))
+    return [(NAMES[st[j]], ts[j], (k[j], ts[j], i[j], p[j])) for j in range(len(ts))]
+
+
+def run(plan, w, batches=1, **opts):
+    rt = fs.SiddhiAppRuntime(plan, **opts)
+    rt.add_callback("O")
+    n = len(w["ts"])
+    cuts = np.linspace(0, n, batches + 1).astype(int)
+    for b in range(batches):
+        s, e = cuts[b], cuts[b + 1]
+        rt.send("A", w["ts"][s:e], [w["k"][s:e], w["ts"][s:e], w["id"][s:e], w["price"][s:e]],
+                streams=w["stream"][s:e])
+        rt.flush()
+    got = engine_rows(rt.collect("O"))
+    rt.shutdown()
+    return got
+
+
+def case(query, n=20000, keys=256, batches=1, **opts):
+    plan = EV3 + query
+    w = three_streams(n, keys)
+    want = oracle_run(plan, events(w)).get("O", [])
+    got = run(plan, w, batches=batches, **opts)
+    assert_same_rows(got, want, query)
+    return len(want)
+
+
+P3 = "partition with (k of A, k of B, k of C) begin "
+
+
+def test_config5_sequence_kleene():
+    m = case(P3 + "from every s1=A[price > 0.25], s2=B[id < 30]+, s3=C[id > 20] within 10 sec "
+             "select s1.k as k, s1.price as p1, s2[last].price as p2, s3.price as p3 "
+             "insert into O; end;", n=60000, keys=64)
+    assert m > 10
+
+
+def test_sequence_two_states_strict_contiguity():
+    m = case(P3 + "from every s1=A[id < 25], s2=B[id >= 25] "
+             "select s1.id as i1, s2.id as i2, s2.ts as t insert into O; end;")
+    assert m > 100
+
+
+def test_sequence_kleene_first_last_and_optional():
+    m = case(P3 + "from every s1=A, s2=B[price > 0.2]+, s3=C? , s4=A[id > 40] within 5 sec "
+             "select s1.id as a, s2.id as b0, s2[last].id as bl, s4.id as d "
+             "insert into O; end;", n=40000, keys=32)
+    assert m > 10
+
+
+def test_three_state_pattern_with_captures():
+    m = case(P3 + "from every s1=A[price > 0.5] -> s2=B[id == s1.id % 7] -> s3=C[price < s1.price] "
+             "within 3 sec select s1.k as k, s1.id as i1, s2.id as i2, s3.price as p3 "
+             "insert into O; end;", n=30000, keys=128)
+    assert m > 50
+
+
+def test_non_every_three_state_pattern_unpartitioned():
+    m = case("from s1=A[id == 3] -> s2=B[id == 4] -> s3=C[id == 5] "
+             "select s1.ts as t1, s2.ts as t2, s3.ts as t3 insert into O;", n=20000, keys=16)
+    assert m == 1
+
+
+def test_sequence_multi_chunk_multi_batch():
+    m = case(P3 + "from every s1=A[price > 0.6], s2=B+, s3=C within 2 sec "
+             "select s1.price as p1, s2[last].price as p2, s3.price as p3 insert into O; end;",
+             n=40000, keys=512, batches=3, chunk_events=4096)
+    assert m > 100
