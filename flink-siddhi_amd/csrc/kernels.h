@@ -193,8 +193,8 @@ void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
 
 constexpr int kFilterThreads = 256;
 constexpr int kFilterItems = 16;          // rows per thread per tile
-constexpr int kPartThreads = 256;
-constexpr int kPartItems = 8;             // tile = 2048 rows
+constexpr int kPartThreads = 512;
+constexpr int kPartItems = 4;             // tile = 2048 rows
 constexpr int kWalkThreads = 512;
 constexpr int kWalkWindow = 1024;         // records per LDS window
 constexpr int kWalkMaxTiles = 2048;       // tiles per chunk

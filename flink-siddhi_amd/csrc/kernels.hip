@@ -286,31 +286,39 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) 
 
 
 // ---- fast partition path helpers (PrefPlan) --------------------------------
-// Raw 16-byte loads of E = 8 consecutive rows of a column of width w; branch
+// Raw 16-byte loads of E consecutive rows of a column of width w; branch
 // free (surplus loads repeat the last address), all issued before any use.
-__device__ __forceinline__ void load_raw8(const void* p, int w, int64_t row, uint4 (&r)[4]) {
+template <int E>
+__device__ __forceinline__ void load_raw(const void* p, int w, int64_t row, uint4 (&r)[E / 2]) {
   const char* b = (const char*)p + row * w;
-  const int nl = w == 8 ? 4 : (w == 4 ? 2 : 1);
+  const int nl = w == 8 ? E / 2 : (w == 4 ? (E / 4 > 0 ? E / 4 : 1) : 1);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = gload4(b + 16 * (i < nl ? i : nl - 1));
+  for (int i = 0; i < E / 2; ++i) r[i] = gload4(b + 16 * (i < nl ? i : nl - 1));
 }
 
-// Decode 8 rows of raw column data into VM words (load_col semantics).
-__device__ __forceinline__ void decode8(const uint4 (&r)[4], int type, uint64_t (&v)[8]) {
-  const uint32_t x[16] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w,
-                          r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+// Decode E rows of raw column data into VM words (load_col semantics).
+template <int E>
+__device__ __forceinline__ void decode(const uint4 (&r)[E / 2], int type, uint64_t (&v)[E]) {
+  uint32_t x[2 * E];
+#pragma unroll
+  for (int i = 0; i < E / 2; ++i) {
+    x[4 * i] = r[i].x;
+    x[4 * i + 1] = r[i].y;
+    x[4 * i + 2] = r[i].z;
+    x[4 * i + 3] = r[i].w;
+  }
   if (type == T_LONG || type == T_DOUBLE) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ((uint64_t)x[2 * e + 1] << 32) | x[2 * e];
+    for (int e = 0; e < E; ++e) v[e] = ((uint64_t)x[2 * e + 1] << 32) | x[2 * e];
   } else if (type == T_BOOL) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ((x[e >> 2] >> (8 * (e & 3))) & 0xffu) ? 1u : 0u;
+    for (int e = 0; e < E; ++e) v[e] = ((x[e >> 2] >> (8 * (e & 3))) & 0xffu) ? 1u : 0u;
   } else if (type == T_FLOAT) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (uint64_t)x[e];
+    for (int e = 0; e < E; ++e) v[e] = (uint64_t)x[e];
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = from_i32((int32_t)x[e]);
+    for (int e = 0; e < E; ++e) v[e] = from_i32((int32_t)x[e]);
   }
 }
 
@@ -427,25 +435,26 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       }
     } else if constexpr (kPf) {
       const int64_t row0 = a.rows.row0 + r0;
-      const bool full = nvalid >= 2 * E;   // 16-byte loads of 1-byte columns stay in bounds
+      const bool full = nvalid >= 16;   // 16-byte loads of 1-byte columns stay in bounds
       // issue every load of the lane's rows before any use
       // (no branches between the loads: a branch join makes the compiler
       // drain them; unused slots repeat column col[0], set by the host)
       const int64_t prev_ld = a.rows.ts[row0 > 0 ? row0 - 1 : row0];
       uint64_t sbytes = 0;
       if (full) {
-        uint4 rt[4], rc[kPref][4];
-        load_raw8(a.rows.ts, 8, row0, rt);
+        uint4 rt[E / 2], rc[kPref][E / 2];
+        load_raw<E>(a.rows.ts, 8, row0, rt);
 #pragma unroll
         for (int q = 0; q < kPref; ++q)
-          load_raw8(a.rows.cols.p[a.pref.col[q]], type_width(a.rows.cols.t[a.pref.col[q]]), row0,
-                    rc[q]);
+          load_raw<E>(a.rows.cols.p[a.pref.col[q]], type_width(a.rows.cols.t[a.pref.col[q]]), row0,
+                      rc[q]);
         const uint8_t* sp = a.rows.stream ? a.rows.stream + row0 : (const uint8_t*)a.rows.ts + row0 * 8;
-        sbytes = *(const __attribute__((address_space(1))) uint64_t*)sp;
-        decode8(rt, T_LONG, tsv);
+        if constexpr (E == 8) sbytes = *(const __attribute__((address_space(1))) uint64_t*)sp;
+        else sbytes = *(const __attribute__((address_space(1))) uint32_t*)sp;
+        decode<E>(rt, T_LONG, tsv);
 #pragma unroll
         for (int q = 0; q < kPref; ++q)
-          if (q < a.pref.n) decode8(rc[q], a.rows.cols.t[a.pref.col[q]], pv[q]);
+          if (q < a.pref.n) decode<E>(rc[q], a.rows.cols.t[a.pref.col[q]], pv[q]);
       } else {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
