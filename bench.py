@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--events", type=int, default=0, help="events per step per GPU")
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--rate", type=int, default=400, help="events per ms")
-    ap.add_argument("--chunk", type=int, default=1 << 22)
+    ap.add_argument("--chunk", type=int, default=1 << 24)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--ingest", choices=["shuffle", "prepartitioned"], default="shuffle",
@@ -250,7 +250,7 @@ def main():
     # per-kernel HIP-event times on the engine's stream over the timed region
     kern = {}
     for k, name in ((L.K_PARTITION, "k_partition"), (L.K_WALK, "k_walk"), (L.K_FILTER, "k_filter"),
-                    (L.K_ROUTE, "k_route")):
+                    (L.K_ROUTE, "k_route"), (L.K_CF_PARTITION, "k_cfpart"), (L.K_CF_WALK, "k_cfwalk")):
         launches = st1.kernel_launches[k] - st0.kernel_launches[k]
         ms = st1.kernel_ms[k] - st0.kernel_ms[k]
         if launches:
@@ -258,17 +258,17 @@ def main():
                           "total_ms": ms}
     m_per_event = (st1.matches_out - st0.matches_out) / float(n * steps)
     if pattern:
-        chunk_events = min(args.chunk, n)
-        walk_launches = kern.get("k_walk", {}).get("launches", 0)
-        per_launch = {"k_walk": PATTERN_OUT_BYTES * (st1.matches_out - st0.matches_out) /
-                      max(1, walk_launches)}
+        # a launch of either pattern kernel processes one chunk of events: its
+        # algorithmic bytes are SURVEY §8(d)'s per-event figure x the chunk
+        alg_per_event = PATTERN_IN_BYTES + PATTERN_OUT_BYTES * m_per_event
+        per_launch = {}
+        for kname in ("k_partition", "k_walk", "k_cfpart", "k_cfwalk"):
+            if kname in kern:
+                per_launch[kname] = alg_per_event * n * steps / kern[kname]["launches"]
         if shuffle_mode:
             # route reads the whole step batch once; the owner's partition pass
             # then reads records, not events (its bytes are not attributed here)
             per_launch["k_route"] = PATTERN_IN_BYTES * n
-        else:
-            per_launch["k_partition"] = PATTERN_IN_BYTES * chunk_events
-        alg_per_event = PATTERN_IN_BYTES + PATTERN_OUT_BYTES * m_per_event
     else:
         per_launch = {"k_filter": (FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event) * n}
         alg_per_event = FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event

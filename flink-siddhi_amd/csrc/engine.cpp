@@ -88,6 +88,10 @@ struct PatternRT {
   int64_t extra_bound = 0;   // pending partials that may still complete
   bool part_vm = true;       // partition pass needs the interpreter
   bool walk_vm = true;       // walk needs the interpreter (g on s1, computed select items)
+  // closed-form fast path (cf_kernels.hip): its own, larger chunk arenas
+  bool cf = false;
+  int64_t cf_chunk = 0;
+  DevBuf cf_recs[2], cf_toff[2];
 };
 
 struct TimedLaunch {
@@ -116,8 +120,8 @@ struct cep_app {
   std::vector<DevBuf> stage;   // host-batch staging columns (+ts, +stream)
   int64_t events_in = 0, matches_out = 0, batches = 0;
   int64_t last_ts = INT64_MIN;
-  int64_t launches[8] = {0};
-  double kernel_ms[8] = {0};
+  int64_t launches[16] = {0};
+  double kernel_ms[16] = {0};
   std::vector<TimedLaunch> timed;
   std::vector<hipEvent_t> event_pool;
   std::vector<std::unique_ptr<char[]>> name_store;
@@ -383,6 +387,30 @@ int create_runtime(cep_app* a) {
     // group-by and N-state / sequence walks live in the VM build of k_walk
     rt.walk_vm = q.g_in_walk || agg || q.nfa;
     for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
+    // closed-form fast path: `every A -> B` with f / g as term lists on the
+    // events' own columns, plain-copy select items, <= 2 captures, <= 512
+    // keys per bucket (CEP_NO_CF=1 forces the general path)
+    {
+      bool ok = p.closed_form && !q.nfa && !agg && !rt.part_vm && !rt.walk_vm && rt.pref.n >= 0 &&
+                p.ncap <= kCfMaxCaps && p.nrec_a <= kPfRec && p.nrec_b <= kPfRec &&
+                kpb <= kCfMaxKeys && (1 << lg) <= kCfMaxBuckets && !std::getenv("CEP_NO_CF");
+      for (auto& it : q.select)
+        ok = ok && (it.src == SRC_KEY || (it.src >= SRC_CAP && it.src < SRC_CAP + kCfMaxCaps) ||
+                    (it.src >= SRC_REC && it.src < SRC_REC + kPfRec));
+      if (ok) {
+        int64_t cc = std::max<int64_t>(a->opt.chunk_events, kCfTile);
+        cc = std::min<int64_t>(cc, (int64_t)kCfMaxTiles * kCfTile);
+        cc = (cc / kCfTile) * kCfTile;
+        const int64_t nt = cc / kCfTile;
+        const int rw = 1 + std::max(p.nrec_a, p.nrec_b);
+        for (int b = 0; b < 2 && ok; ++b)
+          ok = dev_ensure(&rt.cf_recs[b], (size_t)cc * rw * 8 + 16, a->stream, false) &&
+               dev_ensure(&rt.cf_toff[b], (size_t)nt * ((1 << lg) + 1) * 2, a->stream, false);
+        if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
+        rt.cf = true;
+        rt.cf_chunk = cc;
+      }
+    }
     a->pats.push_back(rt);
   }
   if (std::getenv("CEP_STAMPS") && !dev_ensure(&a->stamps, (size_t)2 * 4096 * 16 * 8, a->stream, false))
@@ -439,6 +467,104 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
   return CEP_OK;
 }
 
+// 16-byte loads need every prefetched column (and ts) 16-byte aligned at
+// each lane's first row (lanes start at multiples of 8 rows; 1-byte columns:
+// 8-byte aligned, the hardware takes dword-aligned x4 loads)
+bool pref_aligned(const PrefPlan& pf, const RowsArgs& rows) {
+  auto al = [&](const void* ptr, int w) {
+    const uintptr_t need = w == 1 ? 7u : 15u;
+    return (((uintptr_t)ptr + (uintptr_t)(rows.row0 * w)) & need) == 0;
+  };
+  bool ok = al(rows.ts, 8) && (!rows.stream || al(rows.stream, 1));
+  for (int i = 0; i < pf.n; ++i) {
+    const int c = pf.col[i];
+    ok = ok && al(rows.cols.p[c], type_width(rows.cols.t[c]));
+  }
+  return ok;
+}
+
+// Per-batch layout of the closed-form fast path's records: carried columns
+// whose buffer is the batch's event-ts buffer are rebuilt from the record ts.
+bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf) {
+  const PatternArgs& p = rt.pa;
+  std::memset(cf, 0, sizeof(*cf));
+  int a_phys[kMaxCaps], b_phys[kMaxCaps];
+  int na = 0, nb = 0;
+  auto alias = [&](int col) {
+    return rows.cols.p[col] == (const void*)rows.ts && rows.cols.t[col] == T_LONG;
+  };
+  for (int c = 0; c < p.nrec_a; ++c) {
+    a_phys[c] = alias(p.rec_a[c]) ? -1 : na;
+    if (a_phys[c] >= 0) cf->a_slot[na++] = rt.pref.reca_slot[c];
+  }
+  for (int c = 0; c < p.nrec_b; ++c) {
+    b_phys[c] = alias(p.rec_b[c]) ? -1 : nb;
+    if (b_phys[c] >= 0) cf->b_slot[nb++] = rt.pref.recb_slot[c];
+  }
+  cf->nw = std::max(na, nb);
+  if (cf->nw > 2) return false;
+  for (int w = na; w < 2; ++w) cf->a_slot[w] = 0;
+  for (int w = nb; w < 2; ++w) cf->b_slot[w] = 0;
+  for (int i = 0; i < kMaxCaps; ++i) cf->cap_phys[i] = i < p.ncap ? a_phys[p.cap_from_rec[i]] : 0;
+  for (int c = 0; c < kMaxCaps; ++c) cf->bcol_phys[c] = c < p.nrec_b ? b_phys[c] : 0;
+  return true;
+}
+
+// Closed-form fast path: k_cfpart(c+1) on the side stream overlaps
+// k_cfwalk(c) on the main stream (double-buffered arenas).
+int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
+                   const RowsArgs& rows_all, const CfPlan& cf) {
+  const int P = 1 << rt.pa.buckets_log2;
+  hipEventRecord(a->in_ready, a->stream);
+  hipStreamWaitEvent(a->side, a->in_ready, 0);
+  static const bool no_overlap = std::getenv("CEP_NO_OVERLAP") != nullptr;
+  hipStream_t side = no_overlap ? a->stream : a->side;
+  for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.cf_chunk) {
+    const int b = rt.cur;
+    rt.cur ^= 1;
+    RowsArgs rows = rows_all;
+    rows.row0 = rows_all.row0 + r0;
+    rows.n = std::min<int64_t>(rt.cf_chunk, rows_all.n - r0);
+    if (r0 > 0) rows.prev_ts = INT64_MIN;   // checked inside the kernel via ts[row-1]
+    const int64_t ntiles = (rows.n + kCfTile - 1) / kCfTile;
+    CfPartArgs pa{};
+    pa.rows = rows;
+    pa.pref = rt.pref;
+    pa.pat = rt.pa;
+    pa.cf = cf;
+    pa.chunk_base = (int64_t*)rt.chunk_base[b].p;
+    pa.recs = (uint64_t*)rt.cf_recs[b].p;
+    pa.tile_off = (uint16_t*)rt.cf_toff[b].p;
+    pa.err = (unsigned int*)a->err.p;
+    if (rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
+    {
+      LaunchTimer t(a, CEP_K_CF_PARTITION, side);
+      launch_cf_partition(pa, ntiles, side);
+    }
+    hipEventRecord(rt.part_done[b], side);
+    hipStreamWaitEvent(a->stream, rt.part_done[b], 0);
+    CfWalkArgs wa{};
+    wa.pat = rt.pa;
+    wa.cf = cf;
+    wa.recs = pa.recs;
+    wa.tile_off = pa.tile_off;
+    wa.ntiles = (int32_t)ntiles;
+    wa.chunk_base = (const int64_t*)rt.chunk_base[b].p;
+    wa.khdr = (uint32_t*)rt.khdr.p;
+    wa.kslot = (uint64_t*)rt.kslot.p;
+    wa.kstride = rt.kstride;
+    wa.out = out_args(o, q);
+    wa.err = pa.err;
+    {
+      LaunchTimer t(a, CEP_K_CF_WALK);
+      launch_cf_walk(wa, P, a->stream);
+    }
+    hipEventRecord(rt.walk_done[b], a->stream);
+    rt.used[b] = true;
+  }
+  return CEP_OK;
+}
+
 int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
                 const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
   const Query& q = a->app.queries[rt.q];
@@ -447,6 +573,10 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
   o.bound += rows_all.n;
   int rc = ensure_out_cap(a, o, o.bound);
   if (rc) return rc;
+  if (rt.cf && !in_recs && pref_aligned(rt.pref, rows_all)) {
+    CfPlan cf;
+    if (cf_plan(rt, rows_all, &cf)) return run_pattern_cf(a, rt, q, o, rows_all, cf);
+  }
   const int P = 1 << rt.pa.buckets_log2;
   // the side stream starts after everything already queued on the main stream
   // (host-batch staging copies, earlier queries)
@@ -472,21 +602,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
       pa.in_rec_words = in_rec_words;
       pa.pref.n = -1;
     }
-    if (pa.pref.n >= 0) {
-      // 16-byte loads need every prefetched column (and ts) 16-byte aligned at
-      // each lane's first row (lanes start at multiples of 8 rows)
-      // (1-byte columns: 8-byte aligned; the hardware takes dword-aligned x4 loads)
-      auto al = [&](const void* p, int w) {
-        const uintptr_t need = w == 1 ? 7u : 15u;
-        return (((uintptr_t)p + (uintptr_t)(rows.row0 * w)) & need) == 0;
-      };
-      bool ok = al(rows.ts, 8) && (!rows.stream || al(rows.stream, 1));
-      for (int i = 0; i < pa.pref.n; ++i) {
-        const int c = pa.pref.col[i];
-        ok = ok && al(rows.cols.p[c], type_width(rows.cols.t[c]));
-      }
-      if (!ok) pa.pref.n = -1;
-    }
+    if (pa.pref.n >= 0 && !pref_aligned(pa.pref, rows)) pa.pref.n = -1;
     if (r0 > 0) pa.rows.prev_ts = INT64_MIN;
     pa.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
     pa.pat = rt.pa;
@@ -688,6 +804,8 @@ void cep_destroy(cep_app* a) {
     for (int b = 0; b < 2; ++b) {
       dev_free(&p.recs[b]);
       dev_free(&p.tile_off[b]);
+      dev_free(&p.cf_recs[b]);
+      dev_free(&p.cf_toff[b]);
       dev_free(&p.chunk_base[b]);
     }
   }
@@ -935,7 +1053,7 @@ int cep_stats(cep_app* a, cep_stats_t* s) {
   s->events_in = a->events_in;
   s->matches_out = a->matches_out;
   s->batches = a->batches;
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < 16; ++i) {
     s->kernel_launches[i] = a->launches[i];
     s->kernel_ms[i] = a->kernel_ms[i];
   }

@@ -180,7 +180,60 @@ struct WalkArgs {
   unsigned int* err;
 };
 
+// ------------------------------------------ closed-form fast path (cf_kernels.hip) --
+// `every s1=A[f] -> s2=B[g] within W` with f / g on the events' own columns,
+// at most 2 physical carried words per record and plain-copy select items.
+// Records are 8 + 8*nw bytes:
+//   w0 = ts - chunk ts base (32) | row in tile (13) << 32 | role (3) << 45 | key in bucket (16) << 48
+//   w1.. = physical carried words (A rows: A's, B rows: B's)
+// A carried column whose buffer IS the event-ts buffer is not carried: its
+// value is the record's ts (cap_phys / bcol_phys = -1).
+constexpr int kCfPartThreads = 1024;
+constexpr int kCfItems = 8;                            // rows per lane
+constexpr int kCfTile = kCfPartThreads * kCfItems;     // 8192 rows per tile
+constexpr int kCfWalkThreads = 1024;
+constexpr int kCfWindow = 4096;                        // records per LDS window (nw <= 1)
+constexpr int kCfMaxKeys = 512;                        // keys per bucket
+constexpr int kCfMaxTiles = 2048;                      // chunk <= 16 Mi rows
+constexpr int kCfMaxBuckets = 4096;
+constexpr int kCfMaxCaps = 2;                          // captured words per pending slot
+
+struct CfPlan {
+  int32_t nw;                      // physical carried words per record (0..2)
+  int32_t a_slot[2], b_slot[2];    // prefetch slot of physical word w (A rows / B rows)
+  int32_t cap_phys[kMaxCaps];      // A capture i -> physical word, -1 = the A's event ts
+  int32_t bcol_phys[kMaxCaps];     // B record word c (SRC_REC + c) -> physical word, -1 = ts
+};
+
+struct CfPartArgs {
+  RowsArgs rows;
+  PrefPlan pref;
+  PatternArgs pat;
+  CfPlan cf;
+  int64_t* chunk_base;         // out: {ts, seq} of the chunk's first row
+  uint64_t* recs;              // out: records, tile t at recs + t * kCfTile * (1 + nw)
+  uint16_t* tile_off;          // out: [ntiles][P+1] exclusive bucket offsets per tile
+  unsigned int* err;
+};
+
+struct CfWalkArgs {
+  PatternArgs pat;
+  CfPlan cf;
+  const uint64_t* recs;
+  const uint16_t* tile_off;
+  int32_t ntiles;
+  const int64_t* chunk_base;
+  uint32_t* khdr;              // per-key state, same layout as WalkArgs
+  uint64_t* kslot;
+  int64_t kstride;
+  OutArgs out;
+  uint64_t* stamps;
+  unsigned int* err;
+};
+
 // --------------------------------------------------------------- launchers --
+void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
+void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

@@ -24,6 +24,7 @@
 
 #include "kernels.h"
 #include "vm.h"
+#include "dev_common.h"
 
 namespace cep {
 
@@ -33,48 +34,7 @@ constexpr uint64_t kStatusShift = 62;
 constexpr uint64_t kValueMask = (1ull << 62) - 1;
 constexpr uint16_t kNone16 = 0xffff;
 
-__device__ __forceinline__ void set_err(unsigned int* err, unsigned int bit) {
-  if (err) atomicOr(err, bit);
-}
 
-// Workgroup barrier that orders LDS only.  __syncthreads() also releases
-// global memory, which makes every wave drain its outstanding global loads
-// and stores (s_waitcnt vmcnt(0)) before the barrier; phases that only hand
-// LDS data to each other keep their global traffic in flight with this one.
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Block-wide exclusive scan of one value per thread (blockDim <= 512).
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch /*>=9*/,
-                                                    uint32_t* total) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nwaves = (int)(blockDim.x >> 6);
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) scratch[wave] = x;
-  lds_barrier();
-  if (tid == 0) {
-    uint32_t s = 0;
-    for (int w = 0; w < nwaves; ++w) {
-      uint32_t t = scratch[w];
-      scratch[w] = s;
-      s += t;
-    }
-    scratch[8] = s;
-  }
-  lds_barrier();
-  uint32_t r = scratch[wave] + x - v;
-  *total = scratch[8];
-  lds_barrier();
-  return r;
-}
 
 struct RowEnv {
   const RowsArgs* r;
@@ -285,78 +245,6 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s) 
 }
 
 
-// ---- fast partition path helpers (PrefPlan) --------------------------------
-// Raw 16-byte loads of E consecutive rows of a column of width w; branch
-// free (surplus loads repeat the last address), all issued before any use.
-template <int E>
-__device__ __forceinline__ void load_raw(const void* p, int w, int64_t row, uint4 (&r)[E / 2]) {
-  const char* b = (const char*)p + row * w;
-  const int nl = w == 8 ? E / 2 : (w == 4 ? (E / 4 > 0 ? E / 4 : 1) : 1);
-#pragma unroll
-  for (int i = 0; i < E / 2; ++i) r[i] = gload4(b + 16 * (i < nl ? i : nl - 1));
-}
-
-// Decode E rows of raw column data into VM words (load_col semantics).
-template <int E>
-__device__ __forceinline__ void decode(const uint4 (&r)[E / 2], int type, uint64_t (&v)[E]) {
-  uint32_t x[2 * E];
-#pragma unroll
-  for (int i = 0; i < E / 2; ++i) {
-    x[4 * i] = r[i].x;
-    x[4 * i + 1] = r[i].y;
-    x[4 * i + 2] = r[i].z;
-    x[4 * i + 3] = r[i].w;
-  }
-  if (type == T_LONG || type == T_DOUBLE) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) v[e] = ((uint64_t)x[2 * e + 1] << 32) | x[2 * e];
-  } else if (type == T_BOOL) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) v[e] = ((x[e >> 2] >> (8 * (e & 3))) & 0xffu) ? 1u : 0u;
-  } else if (type == T_FLOAT) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) v[e] = (uint64_t)x[e];
-  } else {
-#pragma unroll
-    for (int e = 0; e < E; ++e) v[e] = from_i32((int32_t)x[e]);
-  }
-}
-
-// Value of prefetched slot `slot` (uniform) for row e.
-template <int N>
-__device__ __forceinline__ uint64_t pick(const uint64_t (&v)[kPref][N], int slot, int e) {
-  // masked OR rather than selects: a select chain on slot == q gets rewritten
-  // into a dynamically indexed (scratch) array access
-  uint64_t x = 0;
-#pragma unroll
-  for (int q = 0; q < kPref; ++q) x |= v[q][e] & (0ull - (uint64_t)(slot == q));
-  return x;
-}
-
-// Term-list predicate over prefetched rows (eval_terms_run without loads).
-template <int N>
-__device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const int32_t* slot,
-                                                    const ColSet& cols,
-                                                    const uint64_t (&vals)[kPref][N]) {
-  uint32_t acc = tl.any ? 0u : ((N >= 32) ? 0xffffffffu : ((1u << N) - 1u));
-  for (int i = 0; i < tl.n; ++i) {
-    const Term& t = tl.t[i];
-    uint64_t v[N];
-#pragma unroll
-    for (int e = 0; e < N; ++e) v[e] = pick<N>(vals, slot[i], e);
-    int ty = (t.coltype == T_BOOL || t.coltype == T_STRING) ? T_INT : t.coltype;
-    uint32_t nullm = 0;
-    if (t.aop) {
-      convert_run<N>(v, ty, t.atype);
-      arith_run<N>(v, t.aop, t.atype, t.aconst, &nullm);
-      ty = t.atype;
-    }
-    convert_run<N>(v, ty, t.ctype);
-    const uint32_t bits = compare_run<N>(v, t.cop, t.ctype, t.cconst) & ~nullm;
-    acc = tl.any ? (acc | bits) : (acc & bits);
-  }
-  return acc;
-}
 
 // =========================================================== k_partition ==
 // Record layout (8-byte words, chunk-relative):
@@ -1378,13 +1266,6 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
   a.khdr[idx] = nh;
 }
 
-// XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
-// §Workgroup dispatch), so consecutive buckets — which share tile-offset
-// cache lines — are given to blocks of one XCD.  Speed only, never correctness.
-__device__ __forceinline__ int xcd_bucket(int bid, int nb) {
-  if (nb < 8 || (nb & 7)) return bid;
-  return (bid & 7) * (nb >> 3) + (bid >> 3);
-}
 
 }  // namespace
 

@@ -124,14 +124,15 @@ typedef struct {
   int64_t events_in;
   int64_t matches_out;
   int64_t batches;
-  int64_t kernel_launches[8];
-  double kernel_ms[8];        /* with cep_options.profile: summed HIP-event time */
+  int64_t kernel_launches[16];
+  double kernel_ms[16];       /* with cep_options.profile: summed HIP-event time */
 } cep_stats_t;
 
 /* Kernel kinds indexing cep_stats_t arrays. */
 enum {
   CEP_K_FILTER = 0, CEP_K_PARTITION = 1, CEP_K_WALK = 2, CEP_K_ROUTE = 3,
-  CEP_K_ORDER = 4, CEP_K_AGG = 5, CEP_K_OTHER = 6
+  CEP_K_ORDER = 4, CEP_K_AGG = 5, CEP_K_OTHER = 6,
+  CEP_K_CF_PARTITION = 7, CEP_K_CF_WALK = 8   /* closed-form fast path (k_cfpart / k_cfwalk) */
 };
 
 /* ---- plan-level calls (no device needed) ------------------------------ */

@@ -1,14 +1,16 @@
 # GPU check: parity tests, smoke, bench (default size), rocprof kernel trace.
+# Every GPU step has its own time limit; the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+  --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-if [ $rc -gt 1 ]; then exit $rc; fi
+if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || exit $?
 if [ -n "${PROF:-}" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || exit $?
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1 || exit $?
 fi
 exit 0
