@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--rate", type=int, default=400, help="events per ms")
     ap.add_argument("--chunk", type=int, default=1 << 24)
+    ap.add_argument("--buckets-log2", type=int, default=0,
+                    help="key buckets = 2^n (0: engine default, <= 512 keys per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--ingest", choices=["shuffle", "prepartitioned"], default="shuffle",
@@ -185,6 +187,8 @@ def main():
         opts = dict(device=local, key_capacity=(args.keys + world - 1) // world,
                     key_stride=world, key_offset=rank, chunk_events=args.chunk,
                     profile=1, ordered_output=0)
+        if args.buckets_log2:
+            opts["buckets_log2"] = args.buckets_log2
     else:
         plan = workload.FILTER_PLAN
         opts = dict(device=local, profile=1, ordered_output=0)

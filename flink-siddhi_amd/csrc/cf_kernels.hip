@@ -37,7 +37,7 @@ namespace cep {
 namespace {
 
 constexpr uint16_t kNoB = 0xffff;
-constexpr int kCfStageBytes = 48 * 1024;    // a tile keeps ~1/3 of its rows at config 3
+constexpr int kCfStageBytes = 36 * 1024;    // a tile keeps ~1/3 of its rows at config 3
 
 // Block-wide exclusive scan of one value per thread, NT <= 1024 threads;
 // scratch holds NT / 64 + 1 words.
@@ -70,6 +70,13 @@ __device__ __forceinline__ uint32_t bscan(uint32_t v, uint32_t* scratch, uint32_
   return r;
 }
 
+// Diagnostics (CEP_STAMPS=1): s_memtime at phase i of block b.
+#define CF_STAMP(i)                                                                 \
+  do {                                                                              \
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096)                          \
+      a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+
 // Record field accessors (w0).
 __device__ __forceinline__ uint32_t rec_row(uint64_t w0) { return (uint32_t)(w0 >> 32) & 0x1fffu; }
 __device__ __forceinline__ uint32_t rec_role(uint64_t w0) { return (uint32_t)(w0 >> 45) & 0x7u; }
@@ -79,17 +86,18 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 
 // ============================================================== k_cfpart ==
 template <int NW>
-__global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
+__global__ __launch_bounds__(kCfPartThreads, 4) void k_cfpart(CfPartArgs a) {   // 2 workgroups per CU
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
   __shared__ uint32_t scratch[NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) uint64_t stage[kStageRecs * RW];
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // P + 1 (dynamic)
   const int tid = threadIdx.x;
-  const int64_t tile = blockIdx.x;
+  const int64_t tile = xcd_tile(blockIdx.x, a.ntiles);
   const PatternArgs& p = a.pat;
   const int lg = p.buckets_log2;
   const int P = 1 << lg;
+  CF_STAMP(0);
   for (int i = tid; i <= P; i += NT) hist[i] = 0;
 
   const int64_t ts_base = a.rows.ts[a.rows.row0];
@@ -97,60 +105,81 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     a.chunk_base[0] = ts_base;
     a.chunk_base[1] = a.rows.seq0 + a.rows.row0;
   }
-  const int64_t r0 = tile * kCfTile + (int64_t)tid * E;   // chunk-relative first row of this lane
-  const int64_t nvalid = a.rows.n - r0;
-  const int64_t row0 = a.rows.row0 + r0;                  // batch row
+  // Lane-interleaved rows: lane l of wave w owns rows w*64*E + 64*e + l
+  // (e < E), so every load instruction reads one contiguous 64-row segment
+  // of a column (fully coalesced).
+  const int lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = tile * kCfTile + (int64_t)wave * 64 * E + lane;   // chunk-relative row of e = 0
+  const int64_t row0 = a.rows.row0 + r0;                                 // batch row of e = 0
+  uint32_t valid = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) valid |= (r0 + 64 * e < a.rows.n ? 1u : 0u) << e;
   uint32_t role_a = 0, role_b = 0;
   uint64_t tsv[E];
   uint64_t pv[kPref][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) tsv[e] = 0;
-  if (nvalid > 0) {
-    // issue every load of the lane's rows before any use (no branches between
-    // them; unused prefetch slots repeat column col[0], set by the host)
-    const bool full = nvalid >= 16;   // 16-byte loads of 1-byte columns stay in bounds
-    const int64_t prev_ld = a.rows.ts[row0 > 0 ? row0 - 1 : row0];
-    uint64_t sbytes = 0;
-    if (full) {
-      uint4 rt[E / 2], rc[kPref][E / 2];
-      load_raw<E>(a.rows.ts, 8, row0, rt);
+  if (valid) {
+    // every load of the lane's rows is issued before any use; unused slots
+    // and the ts alias issue none (uniform branches)
+    uint32_t sb[E];
 #pragma unroll
-      for (int q = 0; q < kPref; ++q)
-        load_raw<E>(a.rows.cols.p[a.pref.col[q]], type_width(a.rows.cols.t[a.pref.col[q]]), row0, rc[q]);
-      if (a.rows.stream) sbytes = *(const __attribute__((address_space(1))) uint64_t*)(a.rows.stream + row0);
-      decode<E>(rt, T_LONG, tsv);
+    for (int e = 0; e < E; ++e) {
+      const bool ok = (valid >> e) & 1u;
+      tsv[e] = ok ? (uint64_t)a.rows.ts[row0 + 64 * e] : 0ull;
+      sb[e] = (ok && a.rows.stream) ? (uint32_t)a.rows.stream[row0 + 64 * e] : (uint32_t)a.rows.input;
+    }
 #pragma unroll
-      for (int q = 0; q < kPref; ++q) decode<E>(rc[q], a.rows.cols.t[a.pref.col[q]], pv[q]);
-    } else {
+    for (int q = 0; q < kPref; ++q) {
+      const int c = a.pref.col[q];
+      const int ty = a.rows.cols.t[c];
+      if (q < a.pref.n && q != a.ts_slot) {
+        const void* base = a.rows.cols.p[c];
+        if (ty == T_LONG || ty == T_DOUBLE) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        tsv[e] = e < nvalid ? (uint64_t)a.rows.ts[row0 + e] : 0;
-        if (a.rows.stream && e < nvalid) sbytes |= (uint64_t)a.rows.stream[row0 + e] << (8 * e);
+          for (int e = 0; e < E; ++e)
+            pv[q][e] = ((valid >> e) & 1u) ? ((const uint64_t*)base)[row0 + 64 * e] : 0ull;
+        } else if (ty == T_BOOL) {
 #pragma unroll
-        for (int q = 0; q < kPref; ++q)
-          pv[q][e] = (q < a.pref.n && e < nvalid)
-                         ? load_col(a.rows.cols.p[a.pref.col[q]], a.rows.cols.t[a.pref.col[q]], row0 + e)
-                         : 0;
+          for (int e = 0; e < E; ++e)
+            pv[q][e] = ((valid >> e) & 1u) ? (((const uint8_t*)base)[row0 + 64 * e] ? 1ull : 0ull) : 0ull;
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const uint32_t v = ((valid >> e) & 1u) ? ((const uint32_t*)base)[row0 + 64 * e] : 0u;
+            pv[q][e] = ty == T_FLOAT ? (uint64_t)v : from_i32((int32_t)v);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) pv[q][e] = 0;
       }
     }
-    int64_t prev = row0 > 0 ? prev_ld : a.rows.prev_ts;
+#pragma unroll
+    for (int q = 0; q < kPref; ++q)
+      if (q == a.ts_slot) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) pv[q][e] = tsv[e];
+      }
     uint32_t is_a = 0, is_b = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int sid = a.rows.stream ? (int)((sbytes >> (8 * e)) & 0xffu) : a.rows.input;
-      if (e < nvalid) {
-        is_a |= (sid == p.a_stream ? 1u : 0u) << e;
-        is_b |= (sid == p.b_stream ? 1u : 0u) << e;
+      if ((valid >> e) & 1u) {
+        is_a |= ((int)sb[e] == p.a_stream ? 1u : 0u) << e;
+        is_b |= ((int)sb[e] == p.b_stream ? 1u : 0u) << e;
       }
     }
-    if (p.within >= 0) {   // event-time order check (`within` pruning relies on it)
+    if (p.within >= 0) {
+      // event-time order check (`within` pruning relies on it): row r - 1 is
+      // held by the previous lane (same e), lane 63 (e - 1), or loaded
+      const int64_t before = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
       bool bad = false;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        if (e < nvalid) {
-          bad |= (int64_t)tsv[e] < prev;
-          prev = (int64_t)tsv[e];
-        }
+        const uint64_t up = __shfl_up(tsv[e], 1, 64);
+        const uint64_t last = e > 0 ? __shfl(tsv[e > 0 ? e - 1 : 0], 63, 64) : 0ull;
+        const int64_t prev = lane > 0 ? (int64_t)up : (e > 0 ? (int64_t)last : before);
+        if ((valid >> e) & 1u) bad |= (int64_t)tsv[e] < prev;
       }
       if (bad) set_err(a.err, ERR_ORDER);
     }
@@ -159,6 +188,7 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     if (is_b) role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
   }
   lds_barrier();   // hist zeroed
+  CF_STAMP(1);
 
   // bits 0-12 rank in tile, 13-24 bucket, 25-26 role (never all ones)
   uint32_t packed[E];
@@ -170,12 +200,8 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B;
     if (!role) continue;
     const int64_t key = a.pref.key_slot >= 0 ? (int64_t)pick<E>(pv, a.pref.key_slot, e) : 0;
-    if (key < 0 || (key % p.key_stride) != p.key_offset) {
-      set_err(a.err, ERR_KEY_RANGE);
-      continue;
-    }
-    const int64_t kfield = key / p.key_stride;
-    if (kfield >= p.key_capacity) {
+    const int64_t kfield = shard_key(key, p.key_stride, p.key_offset);
+    if (kfield < 0 || kfield >= p.key_capacity) {
       set_err(a.err, ERR_KEY_RANGE);
       continue;
     }
@@ -185,13 +211,15 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     packed[e] = (role << 25) | (bucket << 13) | rank;
   }
   lds_barrier();
+  CF_STAMP(2);
   {
-    // exclusive scan of the P bucket counts (P <= 4096: <= 4 per thread)
+    // exclusive scan of the P bucket counts (P <= 4096: <= 8 per thread)
+    constexpr int MAXPER = kCfMaxBuckets / NT;
     const int per = (P + NT - 1) / NT;
-    uint32_t c[4];
+    uint32_t c[MAXPER];
     uint32_t sum = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MAXPER; ++i) {
       const int idx = tid * per + i;
       c[i] = (i < per && idx < P) ? hist[idx] : 0u;
       sum += c[i];
@@ -199,7 +227,7 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     uint32_t total;
     uint32_t off = bscan<NT>(sum, scratch, &total);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MAXPER; ++i) {
       const int idx = tid * per + i;
       if (i < per && idx < P) {
         hist[idx] = off;
@@ -209,6 +237,7 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     if (tid == 0) hist[P] = total;
   }
   lds_barrier();
+  CF_STAMP(3);
   const uint32_t total = hist[P];
   const bool staged = total <= (uint32_t)kStageRecs;   // uniform
   uint64_t* trecs = a.recs + tile * (int64_t)kCfTile * RW;
@@ -220,7 +249,7 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
     const uint32_t slot = hist[b] + rank;
     const int64_t dts = (int64_t)tsv[e] - ts_base;
     if (dts < 0 || dts > 0xffffffffll) set_err(a.err, ERR_ORDER);
-    const uint64_t w0 = (uint64_t)(uint32_t)dts | ((uint64_t)(tid * E + e) << 32) |
+    const uint64_t w0 = (uint64_t)(uint32_t)dts | ((uint64_t)(wave * 64 * E + 64 * e + lane) << 32) |
                         ((uint64_t)role << 45) | ((uint64_t)lkey[e] << 48);
     const bool isa = (role & ROLE_A) != 0;
     uint64_t c0 = 0, c1 = 0;
@@ -238,10 +267,10 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
       if (NW > 1) g[2] = c1;
     }
   }
-  uint16_t* toff = a.tile_off + tile * (int64_t)(P + 1);
-  for (int i = tid; i <= P; i += NT) toff[i] = (uint16_t)hist[i];
+  for (int i = tid; i <= P; i += NT) a.tile_off[(int64_t)i * a.ntiles + tile] = (uint16_t)hist[i];
   if (staged) {
     lds_barrier();
+    CF_STAMP(4);
     // the tile's records are contiguous in HBM: 16-byte coalesced stores
     const int64_t words = (int64_t)total * RW;
     for (int64_t w = 2 * tid; w < words; w += 2 * NT) {
@@ -249,35 +278,44 @@ __global__ __launch_bounds__(kCfPartThreads) void k_cfpart(CfPartArgs a) {
       else trecs[w] = stage[w];
     }
   }
+  CF_STAMP(5);
 }
 
 // ============================================================== k_cfwalk ==
 namespace {
 
-// Records per LDS window: 4096 with <= 1 carried word, 3072 with 2 (LDS).
+// Records per LDS window: the LDS budget keeps 2 workgroups per CU.
 template <int NW>
-constexpr int cf_window() { return NW > 1 ? 3072 : kCfWindow; }
+constexpr int cf_window() { return NW > 1 ? 1536 : kCfWindow; }
 
+// Window layout.  The gather loads only each record's header; the window is
+// sorted by (key, arrival) on compact entries, then the full records are
+// re-read (L2) in sorted order, so every later phase reads LDS contiguously.
 template <int NW, int WIN = cf_window<NW>()>
 struct CfWalkLds {
   uint32_t seg[kCfMaxTiles + 1];       // exclusive prefix of the bucket's segment sizes
-  uint16_t lo[kCfMaxTiles];            // segment start inside each tile's run
-  uint32_t kstart[kCfMaxKeys + 1];     // key runs in `sorted`
+  uint32_t kstart[kCfMaxKeys + 1];     // key runs (sorted positions)
   uint32_t kcur[kCfMaxKeys];           // counting-sort cursors
-  uint32_t wts[WIN];             // ts - chunk ts base
-  uint32_t wseq[WIN];            // chunk-relative row (arrival order)
-  uint16_t wkr[WIN];             // key in bucket | role << 12
-  uint16_t sorted[WIN];          // window slots grouped by key, arrival order per key
+  uint32_t wrec[WIN];                  // arena record index per window slot
   union {
-    struct {
-      uint16_t nextb[WIN];       // sorted position of the next B of the key, or kNoB
-      uint16_t v[WIN];           // output row offset per sorted position
-    };
-    uint16_t rowmap[kCfTile];          // oversize tile: segment index per tile row
+    uint64_t kent[WIN];                // seq << 20 | key << 11 | slot, grouped by key
+    uint64_t scap[NW > 0 ? NW : 1][WIN];   // sorted: physical carried words
   };
-  uint16_t ord[kCfTile];               // oversize tile: segment indices in arrival order
-  uint64_t wcap[NW > 0 ? NW : 1][WIN];   // physical carried words
+  union {
+    uint16_t sorted[WIN];              // window slot per sorted position
+    uint16_t nextb[WIN];               // sorted position of the run's next B, or kNoB
+  };
+  uint32_t sts[WIN];                   // sorted: ts - chunk ts base
+  uint32_t sseq[WIN];                  // sorted: chunk-relative row (arrival order)
+  uint16_t skr[WIN];                   // sorted: key in bucket | role << 12
+  uint16_t v[WIN];                     // output row offset per sorted position
+  uint16_t kfb[kCfMaxKeys];            // first B of the key's run, or kNoB
+  uint16_t klb[kCfMaxKeys];            // last B of the key's run, or kNoB
+  uint32_t klast[kCfMaxKeys];          // ts of the run's last A (if khasa)
+  uint8_t khasa[kCfMaxKeys];
   uint8_t cm[kCfMaxKeys];              // carried partials completed by the key's first B
+  uint32_t obits[kCfTile / 32];        // oversize segment: tile-row presence bitmap
+  uint16_t opre[kCfTile / 32];         // oversize segment: popcount prefix per bitmap word
   uint32_t scratch[kCfWalkThreads / 64 + 1];
   unsigned long long base;
 };
@@ -311,8 +349,10 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
 }  // namespace
 
 template <int NW>
-__global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
+__global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   // 2 workgroups per CU
   constexpr int NT = kCfWalkThreads, RW = 1 + NW, WIN = cf_window<NW>();
+  constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
+  constexpr int PER = WIN / NT;           // window slots per thread
   __shared__ CfWalkLds<NW> L;
   const int tid = threadIdx.x;
   const PatternArgs& p = a.pat;
@@ -325,6 +365,7 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
   const int sw = p.slot_words;   // 2 + ncap
   const int S = p.pending_slots;
   const int64_t W = p.within;
+  CF_STAMP(0);
 
   // ---- key lane (tid < kpb): pending count + slots 0 / 1 in registers,
   // loaded now so the state read overlaps the gather below
@@ -333,45 +374,71 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
   uint64_t* ksl = a.kslot + kidx;   // slot j word w: ksl[(j * sw + w) * ks]
   uint32_t hdr = klane ? a.khdr[kidx] : 0u;
   int n = (int)(hdr & 0xffu);
-  // (named scalars, not an array: a dynamically indexed array lands in scratch)
-  uint64_t s00 = 0, s01 = 0, s02 = 0, s03 = 0, s10 = 0, s11 = 0, s12 = 0, s13 = 0;
-  auto load_regs = [&]() {
-    s00 = n > 0 ? ksl[0] : 0ull;
-    s01 = n > 0 ? ksl[ks] : 0ull;
-    s02 = n > 0 && sw > 2 ? ksl[2 * ks] : 0ull;
-    s03 = n > 0 && sw > 3 ? ksl[3 * ks] : 0ull;
-    s10 = n > 1 ? ksl[(int64_t)sw * ks] : 0ull;
-    s11 = n > 1 ? ksl[(int64_t)(sw + 1) * ks] : 0ull;
-    s12 = n > 1 && sw > 2 ? ksl[(int64_t)(sw + 2) * ks] : 0ull;
-    s13 = n > 1 && sw > 3 ? ksl[(int64_t)(sw + 3) * ks] : 0ull;
+  // Slots 0 / 1 (ts + captures) live in registers for the whole kernel: read
+  // once here, rewritten by the commit of each window (named scalars: a
+  // dynamically indexed array lands in scratch).  Word 1 of a slot (the A's
+  // arrival number) is not needed by the closed form and is neither read nor
+  // written here; slots >= 2 stay in HBM.
+  const bool c1 = sw > 2, c2 = sw > 3;
+  uint64_t t0r = 0, t1r = 0, a0c0 = 0, a0c1 = 0, a1c0 = 0, a1c1 = 0;
+  if (n > 0) {
+    t0r = ksl[0];
+    if (c1) a0c0 = ksl[2 * ks];
+    if (c2) a0c1 = ksl[3 * ks];
+  }
+  if (n > 1) {
+    t1r = ksl[(int64_t)sw * ks];
+    if (c1) a1c0 = ksl[(int64_t)(sw + 2) * ks];
+    if (c2) a1c1 = ksl[(int64_t)(sw + 3) * ks];
+  }
+  // (masked selects: a select chain on j / w is turned into a stack array)
+  auto slot_word = [&](int j, int w) -> uint64_t {
+    if (j >= 2) return ksl[((int64_t)j * sw + w) * ks];
+    const uint64_t m0 = 0ull - (uint64_t)(j == 0), m1 = ~m0;
+    const uint64_t w0 = 0ull - (uint64_t)(w == 0), w2 = 0ull - (uint64_t)(w == 2);
+    const uint64_t w3 = 0ull - (uint64_t)(w == 3);
+    return (m0 & ((t0r & w0) | (a0c0 & w2) | (a0c1 & w3))) |
+           (m1 & ((t1r & w0) | (a1c0 & w2) | (a1c1 & w3)));
   };
-  load_regs();
   const int64_t ts_base = a.chunk_base[0];
   const int64_t seq_base = a.chunk_base[1];
   for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
 
-  // ---- the bucket's segment in every tile -> exclusive prefix over tiles
+  // ---- the bucket's segment in every tile (two contiguous rows of the
+  // bucket-major offset table) -> exclusive prefix over tiles; this thread's
+  // segment starts stay in registers for the gather
+  uint32_t lop[TPT / 2];   // packed u16 segment starts of tiles tid*TPT + i
   {
-    constexpr int TPT = kCfMaxTiles / NT;
     uint32_t cnt[TPT];
     uint32_t sum = 0;
+    const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
+    const uint16_t* rhi = rlo + ntiles;
+    const int tb = tid * TPT;
+    if ((ntiles & 7) == 0 && tb + TPT <= ntiles) {
+      const uint4 x = gload4(rlo + tb), y = gload4(rhi + tb);
+      lop[0] = x.x; lop[1] = x.y; lop[2] = x.z; lop[3] = x.w;
+      const uint32_t ys[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      const int t = tid * TPT + i;
-      cnt[i] = 0;
-      if (t < ntiles) {
-        const uint16_t* o = a.tile_off + (int64_t)t * (P + 1) + bucket;
-        const uint32_t lo = o[0], hi = o[1];
-        L.lo[t] = (uint16_t)lo;
-        cnt[i] = hi - lo;
+      for (int i = 0; i < TPT; ++i)
+        cnt[i] = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+    } else {
+#pragma unroll
+      for (int i = 0; i < TPT / 2; ++i) lop[i] = 0;
+#pragma unroll
+      for (int i = 0; i < TPT; ++i) {
+        const int t = tb + i;
+        const uint32_t lo = t < ntiles ? rlo[t] : 0u;
+        lop[i >> 1] |= lo << (16 * (i & 1));
+        cnt[i] = t < ntiles ? (uint32_t)rhi[t] - lo : 0u;
       }
-      sum += cnt[i];
     }
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) sum += cnt[i];
     uint32_t total;
     uint32_t off = bscan<NT>(sum, L.scratch, &total);
 #pragma unroll
     for (int i = 0; i < TPT; ++i) {
-      const int t = tid * TPT + i;
+      const int t = tb + i;
       if (t < ntiles) {
         L.seg[t] = off;
         off += cnt[i];
@@ -380,38 +447,18 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
     if (tid == 0) L.seg[ntiles] = total;
   }
   lds_barrier();
+  CF_STAMP(1);
   const uint32_t nall = L.seg[ntiles];
-
-  // the closed form keeps, per key and window, `n` pending partials (slots
-  // 0..n-1, ts-ordered) and walks the window's records of the key
-  auto slot_word = [&](int j, int w) -> uint64_t {
-    if (j >= 2) return ksl[((int64_t)j * sw + w) * ks];
-    const uint64_t m0 = 0ull - (uint64_t)(w == 0), m1 = 0ull - (uint64_t)(w == 1);
-    const uint64_t m2 = 0ull - (uint64_t)(w == 2), m3 = 0ull - (uint64_t)(w == 3);
-    return j == 0 ? ((s00 & m0) | (s01 & m1) | (s02 & m2) | (s03 & m3))
-                  : ((s10 & m0) | (s11 & m1) | (s12 & m2) | (s13 & m3));
-  };
-
-  // One LDS record per window position.
-  auto put = [&](uint32_t pos, uint32_t trow, const uint4 x, uint64_t y) {
-    const uint64_t w0 = ((uint64_t)x.y << 32) | x.x;
-    const uint32_t k = rec_key(w0);
-    L.wts[pos] = x.x;
-    L.wseq[pos] = trow + rec_row(w0);
-    L.wkr[pos] = (uint16_t)(k | (rec_role(w0) << 12));
-    if (NW > 0) L.wcap[0][pos] = ((uint64_t)x.w << 32) | x.z;
-    if (NW > 1) L.wcap[NW > 1 ? 1 : 0][pos] = y;
-    atomicAdd(&L.kstart[k + 1], 1u);
-  };
 
   // Windows are runs of whole tiles: a tile's segment is in bucket-rank
   // order, not arrival order, so a window never splits one — except a single
   // segment larger than a window (a key holding most of a tile), which is
-  // first put in arrival order in LDS (`ord`; rows are unique in a tile) and
-  // then walked in pieces.
+  // walked in pieces of consecutive arrival rank (rows are unique in a tile:
+  // rank = popcount of the row-presence bitmap below the row).
   int t0 = 0;
+  int wi = 0;               // window index (diagnostic stamps: windows 0 and 1)
   bool over = false;        // tile t0's segment is being walked in pieces
-  uint32_t piece = 0;       // next piece start (index into ord)
+  uint32_t piece = 0;       // next piece's first arrival rank
   while (t0 < ntiles && L.seg[t0] < nall) {
     int t1 = t0;
     uint32_t nw;
@@ -425,66 +472,74 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
       }
       t1 = lo;
       if (t1 == t0) {
-        // ---- oversize segment: arrival order by a scatter over tile rows
         over = true;
         piece = 0;
         const uint32_t c = L.seg[t0 + 1] - L.seg[t0];
-        const uint64_t* tr = a.recs + ((int64_t)t0 * kCfTile + L.lo[t0]) * RW;
-        for (int r = tid; r < kCfTile; r += NT) L.rowmap[r] = kNoB;
+        const uint64_t* tr = a.recs + ((int64_t)t0 * kCfTile + a.tile_off[(int64_t)bucket * ntiles + t0]) * RW;
+        for (int w = tid; w < kCfTile / 32; w += NT) L.obits[w] = 0;
         lds_barrier();
-        for (uint32_t j = tid; j < c; j += NT) L.rowmap[rec_row(tr[(int64_t)j * RW])] = (uint16_t)j;
-        lds_barrier();
-        constexpr int RPT = kCfTile / NT;
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) cnt += L.rowmap[tid * RPT + i] != kNoB ? 1u : 0u;
-        uint32_t total;
-        uint32_t off = bscan<NT>(cnt, L.scratch, &total);
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-          const uint16_t j = L.rowmap[tid * RPT + i];
-          if (j != kNoB) L.ord[off++] = j;
+        for (uint32_t j = tid; j < c; j += NT) {
+          const uint32_t row = rec_row(tr[(int64_t)j * RW]);
+          atomicOr(&L.obits[row >> 5], 1u << (row & 31));
         }
+        lds_barrier();
+        const uint32_t pc = tid < kCfTile / 32 ? (uint32_t)__popc(L.obits[tid]) : 0u;
+        uint32_t total;
+        const uint32_t off = bscan<NT>(pc, L.scratch, &total);
+        if (tid < kCfTile / 32) L.opre[tid] = (uint16_t)off;
         lds_barrier();
       }
     }
+    // ---- window slot -> arena record index (LDS only)
     if (over) {
       const uint32_t c = L.seg[t0 + 1] - L.seg[t0];
       nw = min((uint32_t)WIN, c - piece);
-      const uint64_t* tr = a.recs + ((int64_t)t0 * kCfTile + L.lo[t0]) * RW;
-      const uint32_t trow = (uint32_t)t0 * (uint32_t)kCfTile;
-      for (uint32_t q = tid; q < nw; q += NT) {
-        const uint64_t* r = tr + (int64_t)L.ord[piece + q] * RW;
-        put(q, trow, gload4(r), NW > 1 ? r[2] : 0ull);
+      const int64_t g0 = (int64_t)t0 * kCfTile + a.tile_off[(int64_t)bucket * ntiles + t0];
+      const uint64_t* tr = a.recs + g0 * RW;
+      for (uint32_t j = tid; j < c; j += NT) {
+        const uint32_t row = rec_row(tr[(int64_t)j * RW]);
+        const uint32_t rank = L.opre[row >> 5] + (uint32_t)__popc(L.obits[row >> 5] & ((1u << (row & 31)) - 1u));
+        if (rank >= piece && rank < piece + nw) L.wrec[rank - piece] = (uint32_t)(g0 + j);
       }
     } else {
       nw = L.seg[t1] - L.seg[t0];
-      // ---- gather whole tiles (tile order = arrival order)
       const uint32_t wb = L.seg[t0];
-      constexpr int TPT = kCfMaxTiles / NT;
 #pragma unroll
       for (int i = 0; i < TPT; ++i) {
         const int t = tid * TPT + i;
         if (t < t0 || t >= t1) continue;
         const uint32_t s0 = L.seg[t], s1 = L.seg[t + 1];
-        if (s0 >= s1) continue;
-        const uint32_t trow = (uint32_t)t * (uint32_t)kCfTile;
-        const uint64_t* tr = a.recs + ((int64_t)t * kCfTile + L.lo[t]) * RW;
-        for (uint32_t g = s0; g < s1; g += 2) {
-          // two independent record loads in flight per step
-          const bool two = g + 1 < s1;
-          const uint64_t* r = tr + (int64_t)(g - s0) * RW;
-          const uint4 x0 = gload4(r);
-          const uint4 x1 = two ? gload4(r + RW) : make_uint4(0, 0, 0, 0);
-          const uint64_t y0 = NW > 1 ? r[2] : 0ull;
-          const uint64_t y1 = (NW > 1 && two) ? r[RW + 2] : 0ull;
-          put(g - wb, trow, x0, y0);
-          if (two) put(g + 1 - wb, trow, x1, y1);
-        }
+        const uint32_t g0 = (uint32_t)t * (uint32_t)kCfTile + ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+        for (uint32_t g = s0; g < s1; ++g) L.wrec[g - wb] = g0 + (g - s0);
+      }
+    }
+    if (klane) {
+      L.kfb[tid] = kNoB;
+      L.klb[tid] = kNoB;
+      L.khasa[tid] = 0;
+    }
+    lds_barrier();
+    // ---- headers of every record of the window in flight at once; key counts
+    uint32_t hk[PER], hs[PER];
+    {
+      uint64_t h[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t q = tid + i * NT;
+        h[i] = q < nw ? a.recs[(int64_t)L.wrec[q] * RW] : 0ull;
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t q = tid + i * NT;
+        hk[i] = rec_key(h[i]);
+        hs[i] = (L.wrec[q < nw ? q : 0] & ~(uint32_t)(kCfTile - 1)) + rec_row(h[i]);
+        if (q < nw) atomicAdd(&L.kstart[hk[i] + 1], 1u);
       }
     }
     lds_barrier();
-    // ---- counting sort by key
+    CF_STAMP(wi * 8 + 2);
+    // ---- counting sort by key of (seq, key, slot) entries, then each entry's
+    // arrival rank inside its key run -> sorted position
     {
       const uint32_t c = tid < kpb ? L.kstart[tid + 1] : 0u;
       uint32_t total;
@@ -496,50 +551,95 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
       if (tid == 0) L.kstart[kpb] = total;
     }
     lds_barrier();
-    for (uint32_t w = tid; w < nw; w += NT) {
-      const uint32_t slot = atomicAdd(&L.kcur[L.wkr[w] & 0xfffu], 1u);
-      L.sorted[slot] = (uint16_t)w;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t q = tid + i * NT;
+      if (q >= nw) continue;
+      const uint32_t slot = atomicAdd(&L.kcur[hk[i]], 1u);
+      L.kent[slot] = ((uint64_t)hs[i] << 20) | ((uint64_t)hk[i] << 11) | q;
     }
     lds_barrier();
-
-    // ---- key lanes: arrival order per run, next-B links, carried matches
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t s = tid + i * NT;
+      if (s >= nw) continue;
+      const uint64_t e = L.kent[s];
+      const uint32_t k = (uint32_t)(e >> 11) & 0x1ffu;
+      const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
+      uint32_t rank = 0;
+      for (uint32_t j = r0; j < r1; ++j) rank += (L.kent[j] >> 20) < (e >> 20) ? 1u : 0u;
+      L.sorted[r0 + rank] = (uint16_t)(e & 0x7ffu);
+    }
+    lds_barrier();
+    // ---- full records re-read (L2) in sorted order -> contiguous LDS arrays
+    {
+      uint4 x[PER];
+      uint64_t y[PER];
+      uint32_t gr[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t s = tid + i * NT;
+        x[i] = make_uint4(0, 0, 0, 0);
+        y[i] = 0;
+        gr[i] = 0;
+        if (s < nw) {
+          gr[i] = L.wrec[L.sorted[s]];
+          const uint64_t* r = a.recs + (int64_t)gr[i] * RW;
+          x[i] = gload4(r);
+          if (NW > 1) y[i] = r[2];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t s = tid + i * NT;
+        if (s >= nw) continue;
+        const uint64_t w0 = ((uint64_t)x[i].y << 32) | x[i].x;
+        L.sts[s] = x[i].x;
+        L.sseq[s] = (gr[i] & ~(uint32_t)(kCfTile - 1)) + rec_row(w0);
+        L.skr[s] = (uint16_t)(rec_key(w0) | (rec_role(w0) << 12));
+        if (NW > 0) L.scap[0][s] = ((uint64_t)x[i].w << 32) | x[i].z;
+        if (NW > 1) L.scap[NW > 1 ? 1 : 0][s] = y[i];
+      }
+    }
+    lds_barrier();
+    CF_STAMP(wi * 8 + 3);
+    // ---- per sorted position: next B of the run, first / last B, last A
+#pragma unroll 1
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t s = tid + i * NT;
+      if (s >= nw) continue;
+      const uint32_t kr = L.skr[s];
+      const uint32_t k = kr & 0xfffu, role = kr >> 12;
+      const uint32_t r1 = L.kstart[k + 1];
+      uint16_t nb = kNoB;
+      bool later_a = false;
+      for (uint32_t j = s + 1; j < r1; ++j) {
+        const uint32_t rj = (uint32_t)L.skr[j] >> 12;
+        later_a |= (rj & ROLE_A) != 0;
+        if (rj & ROLE_B) {
+          if (nb == kNoB) nb = (uint16_t)j;
+          if (later_a || !(role & ROLE_A)) break;
+        }
+      }
+      L.nextb[s] = nb;
+      if ((role & ROLE_A) && !later_a) {
+        L.klast[k] = L.sts[s];
+        L.khasa[k] = 1;
+      }
+      if ((role & ROLE_B) && nb == kNoB) L.klb[k] = (uint16_t)s;
+      if (s == L.kstart[k]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)s : nb;
+    }
+    lds_barrier();
+    // ---- key lanes: carried partials completed by the run's first B
     uint32_t r0 = 0, r1 = 0;
-    int fb = -1, lb = -1;            // first / last B (sorted positions)
-    int64_t last_a_ts = INT64_MIN;
     int cfirst = 0, cm = 0;
+    uint64_t e00 = 0, e01 = 0, e10 = 0, e11 = 0;
     if (klane) {
       r0 = L.kstart[tid];
       r1 = L.kstart[tid + 1];
-      const uint32_t len = r1 - r0;
-      if (len > 1) {
-        for (uint32_t gap = len > 64 ? len / 3 : 1;; gap = gap / 3 ? gap / 3 : 1) {
-          for (uint32_t i = r0 + gap; i < r1; ++i) {
-            const uint16_t x = L.sorted[i];
-            const uint32_t sx = L.wseq[x];
-            uint32_t j = i;
-            while (j >= r0 + gap && L.wseq[L.sorted[j - gap]] > sx) {
-              L.sorted[j] = L.sorted[j - gap];
-              j -= gap;
-            }
-            L.sorted[j] = x;
-          }
-          if (gap == 1) break;
-        }
-      }
-      uint16_t nb = kNoB;
-      for (uint32_t q = r1; q-- > r0;) {
-        const uint16_t x = L.sorted[q];
-        const uint32_t role = (uint32_t)L.wkr[x] >> 12;
-        L.nextb[q] = nb;
-        if (role & ROLE_B) {
-          nb = (uint16_t)q;
-          if (lb < 0) lb = (int)q;
-        }
-        if ((role & ROLE_A) && last_a_ts == INT64_MIN) last_a_ts = ts_base + (int64_t)L.wts[x];
-      }
-      fb = nb == kNoB ? -1 : (int)nb;
-      if (r1 > r0 && fb >= 0 && n > 0) {
-        const int64_t tb = ts_base + (int64_t)L.wts[L.sorted[fb]];
+      const uint16_t fb = L.kfb[tid];
+      if (r1 > r0 && fb != kNoB && n > 0) {
+        const int64_t tb = ts_base + (int64_t)L.sts[fb];
         cfirst = n;
         for (int j = 0; j < n; ++j) {
           const int64_t d = tb - (int64_t)slot_word(j, 0);
@@ -551,12 +651,22 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
         cm = n - cfirst;
       }
       L.cm[tid] = (uint8_t)cm;
+      // captures of the first two completed carried partials (registers
+      // unless the partial sits in slot >= 2)
+      if (cm > 0) {
+        e00 = c1 ? slot_word(cfirst, 2) : 0ull;
+        e01 = c2 ? slot_word(cfirst, 3) : 0ull;
+      }
+      if (cm > 1) {
+        e10 = c1 ? slot_word(cfirst + 1, 2) : 0ull;
+        e11 = c2 ? slot_word(cfirst + 1, 3) : 0ull;
+      }
     }
     lds_barrier();
+    CF_STAMP(wi * 8 + 4);
 
     // ---- match flag per sorted position (+ carried matches at run start)
     {
-      constexpr int PER = WIN / NT;
       uint32_t vals[PER];
       uint32_t sum = 0;
 #pragma unroll
@@ -564,11 +674,11 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
         const uint32_t q = tid * PER + i;
         uint32_t val = 0;
         if (q < nw) {
-          const uint16_t x = L.sorted[q];
-          const uint32_t kr = L.wkr[x];
+          const uint32_t kr = L.skr[q];
           const uint32_t k = kr & 0xfffu;
-          if (((kr >> 12) & ROLE_A) && L.nextb[q] != kNoB) {
-            const int64_t d = (int64_t)L.wts[L.sorted[L.nextb[q]]] - (int64_t)L.wts[x];
+          const uint16_t nb = L.nextb[q];
+          if (((kr >> 12) & ROLE_A) && nb != kNoB) {
+            const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
             val = (W < 0 || (d < 0 ? -d : d) <= W) ? 1u : 0u;
           }
           if (q == L.kstart[k]) val += L.cm[k];
@@ -580,89 +690,108 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
       uint32_t off = bscan<NT>(sum, L.scratch, &total);
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        const uint32_t q = tid * PER + i;
-        if (q < (uint32_t)WIN) L.v[q] = (uint16_t)off;
+        L.v[tid * PER + i] = (uint16_t)off;
         off += vals[i];
       }
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
     }
     lds_barrier();
+    CF_STAMP(wi * 8 + 5);
     const unsigned long long base = L.base;
 
     // ---- emit record matches (lane per sorted position; LDS reads + stores)
-    for (uint32_t q = tid; q < nw; q += NT) {
-      const uint16_t x = L.sorted[q];
-      const uint32_t kr = L.wkr[x];
-      if (!((kr >> 12) & ROLE_A) || L.nextb[q] == kNoB) continue;
-      const uint16_t xb = L.sorted[L.nextb[q]];
-      const int64_t d = (int64_t)L.wts[xb] - (int64_t)L.wts[x];
+    const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
+#pragma unroll 1
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t q = tid + i * NT;
+      if (q >= nw) continue;
+      const uint32_t kr = L.skr[q];
+      const uint16_t nb = L.nextb[q];
+      if (!((kr >> 12) & ROLE_A) || nb == kNoB) continue;
+      const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
       if (W >= 0 && (d < 0 ? -d : d) > W) continue;
       const uint32_t k = kr & 0xfffu;
       const uint32_t extra = q == L.kstart[k] ? L.cm[k] : 0u;
-      const int64_t ats = ts_base + (int64_t)L.wts[x];
-      const int64_t bts = ts_base + (int64_t)L.wts[xb];
-      const uint64_t a0 = NW > 0 ? L.wcap[0][x] : 0ull, a1 = NW > 1 ? L.wcap[NW > 1 ? 1 : 0][x] : 0ull;
-      const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
-      const uint64_t c0 = cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1);
-      const uint64_t c1 = cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1);
+      const int64_t ats = ts_base + (int64_t)L.sts[q];
+      const int64_t bts = ts_base + (int64_t)L.sts[nb];
+      const uint64_t a0 = NW > 0 ? L.scap[0][q] : 0ull, a1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][q] : 0ull;
+      const uint64_t x0 = cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1);
+      const uint64_t x1 = cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1);
       const int64_t kl = ((int64_t)k << lg) | bucket;
-      cf_emit(a, base + L.v[q] + extra, kl * p.key_stride + p.key_offset, c0, c1,
-              NW > 0 ? L.wcap[0][xb] : 0ull, NW > 1 ? L.wcap[NW > 1 ? 1 : 0][xb] : 0ull, bts,
-              seq_base + (int64_t)L.wseq[xb]);
+      cf_emit(a, base + L.v[q] + extra, kl * p.key_stride + p.key_offset, x0, x1,
+              NW > 0 ? L.scap[0][nb] : 0ull, NW > 1 ? L.scap[NW > 1 ? 1 : 0][nb] : 0ull, bts,
+              seq_base + (int64_t)L.sseq[nb]);
     }
+    CF_STAMP(wi * 8 + 6);
 
     // ---- key lanes: carried matches, survivors, state commit
     if (klane && r1 > r0) {
       const int64_t kl = ((int64_t)tid << lg) | bucket;
       const int64_t kv = kl * p.key_stride + p.key_offset;
+      const uint16_t fb = L.kfb[tid], lb = L.klb[tid];
       if (cm) {
-        const uint16_t xb = L.sorted[fb];
-        const int64_t bts = ts_base + (int64_t)L.wts[xb];
-        const uint64_t b0 = NW > 0 ? L.wcap[0][xb] : 0ull, b1 = NW > 1 ? L.wcap[NW > 1 ? 1 : 0][xb] : 0ull;
+        const int64_t bts = ts_base + (int64_t)L.sts[fb];
+        const uint64_t b0 = NW > 0 ? L.scap[0][fb] : 0ull, b1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][fb] : 0ull;
         for (int j = 0; j < cm; ++j) {
           const int js = cfirst + j;
-          cf_emit(a, base + L.v[r0] + j, kv, slot_word(js, 2), slot_word(js, 3), b0, b1, bts,
-                  seq_base + (int64_t)L.wseq[xb]);
+          const uint64_t x0 = j == 0 ? e00 : (j == 1 ? e10 : (c1 ? slot_word(js, 2) : 0ull));
+          const uint64_t x1 = j == 0 ? e01 : (j == 1 ? e11 : (c2 ? slot_word(js, 3) : 0ull));
+          cf_emit(a, base + L.v[r0] + j, kv, x0, x1, b0, b1, bts, seq_base + (int64_t)L.sseq[fb]);
         }
       }
-      const bool prune = W >= 0 && last_a_ts != INT64_MIN;
+      const bool prune = W >= 0 && L.khasa[tid];
+      const int64_t last_a_ts = ts_base + (int64_t)L.klast[tid];
+      // new pending list, built in place: (no B in the run) the carried
+      // partials minus the pruned prefix, then the starts after the last B
+      // minus pruned ones.  Slot j is written only after every old slot it
+      // could overwrite has been read (old slot j' >= j is read at step j').
       int nn = 0;
-      if (lb < 0) {
-        // no B: the carried partials survive, minus those pruned by the
-        // run's last start (ts-ordered, so a prefix)
+      auto put_slot = [&](uint64_t ts, uint64_t x0, uint64_t x1) {
+        const uint64_t m0 = 0ull - (uint64_t)(nn == 0), m1 = 0ull - (uint64_t)(nn == 1);
+        t0r = (ts & m0) | (t0r & ~m0);
+        a0c0 = (x0 & m0) | (a0c0 & ~m0);
+        a0c1 = (x1 & m0) | (a0c1 & ~m0);
+        t1r = (ts & m1) | (t1r & ~m1);
+        a1c0 = (x0 & m1) | (a1c0 & ~m1);
+        a1c1 = (x1 & m1) | (a1c1 & ~m1);
+        uint64_t* dst = ksl + (int64_t)nn * sw * ks;
+        dst[0] = ts;
+        if (c1) dst[2 * ks] = x0;
+        if (c2) dst[3 * ks] = x1;
+        ++nn;
+      };
+      if (lb == kNoB) {
         int drop = 0;
         while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
-        if (drop) {
-          for (int j = drop; j < n; ++j)
-            for (int w = 0; w < sw; ++w) ksl[((int64_t)(j - drop) * sw + w) * ks] = slot_word(j, w);
+        if (drop == 0) {
+          nn = n;   // unchanged, in place
+        } else {
+          for (int j = drop; j < n; ++j) {
+            const uint64_t ts = slot_word(j, 0);
+            const uint64_t x0 = c1 ? slot_word(j, 2) : 0ull, x1 = c2 ? slot_word(j, 3) : 0ull;
+            put_slot(ts, x0, x1);
+          }
         }
-        nn = n - drop;
       }
       // partials created after the last B (a record that is both B and A
       // starts a partial after completing others)
-      for (uint32_t q = (lb < 0 ? r0 : (uint32_t)lb); q < r1; ++q) {
-        const uint16_t x = L.sorted[q];
-        if (!((L.wkr[x] >> 12) & ROLE_A)) continue;
-        const int64_t ats = ts_base + (int64_t)L.wts[x];
+      for (uint32_t q = (lb == kNoB ? r0 : (uint32_t)lb); q < r1; ++q) {
+        if (!((L.skr[q] >> 12) & ROLE_A)) continue;
+        const int64_t ats = ts_base + (int64_t)L.sts[q];
         if (prune && last_a_ts - ats > W) continue;
         if (nn >= S) {
           set_err(a.err, ERR_PENDING);
           break;
         }
-        const uint64_t a0 = NW > 0 ? L.wcap[0][x] : 0ull, a1 = NW > 1 ? L.wcap[NW > 1 ? 1 : 0][x] : 0ull;
-        uint64_t* dst = ksl + (int64_t)nn * sw * ks;
-        dst[0] = (uint64_t)ats;
-        dst[ks] = (uint64_t)(seq_base + (int64_t)L.wseq[x]);
-        for (int c = 0; c < sw - 2; ++c) {
-          const int cp = a.cf.cap_phys[c];
-          dst[(2 + c) * ks] = cp < 0 ? (uint64_t)ats : (cp == 0 ? a0 : a1);
-        }
-        ++nn;
+        const uint64_t a0 = NW > 0 ? L.scap[0][q] : 0ull, a1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][q] : 0ull;
+        put_slot((uint64_t)ats, cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1),
+                 cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
       }
       n = nn;
       hdr = (hdr & ~0xffu) | (uint32_t)nn;
       a.khdr[kidx] = hdr;
     }
+    CF_STAMP(wi * 8 + 7);
     if (over) {
       piece += nw;
       if (piece >= L.seg[t0 + 1] - L.seg[t0]) {
@@ -673,10 +802,10 @@ __global__ __launch_bounds__(kCfWalkThreads) void k_cfwalk(CfWalkArgs a) {
       t0 = t1;
     }
     if (!over && (t0 >= ntiles || L.seg[t0] >= nall)) break;
-    // next window: the key lanes re-read the slots they just wrote; the LDS
-    // arrays are reused
-    __syncthreads();
-    if (klane) load_regs();
+    wi = 1;
+    // next window: the LDS arrays are reused (a key's slots >= 2 are read
+    // back only by the lane that wrote them)
+    lds_barrier();
     for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
     lds_barrier();
   }

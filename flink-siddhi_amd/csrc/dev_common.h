@@ -51,6 +51,17 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
   return r;
 }
 
+// Shard-local dense key of partition key `key` (cep_options key_stride /
+// key_offset: this shard owns key % stride == offset), or -1 when the key is
+// negative or not owned.  stride == 1 (one shard) skips the division; else a
+// 32-bit division (keys are int attributes).
+__device__ __forceinline__ int64_t shard_key(int64_t key, int32_t stride, int32_t offset) {
+  if (stride == 1) return (key < 0 || offset != 0) ? -1 : key;
+  if (key < 0 || key > 0xffffffffll) return -1;
+  const uint32_t k = (uint32_t)key, q = k / (uint32_t)stride;
+  return (k - q * (uint32_t)stride) == (uint32_t)offset ? (int64_t)q : -1;
+}
+
 // ---- fast partition path helpers (PrefPlan) --------------------------------
 // Raw 16-byte loads of E consecutive rows of a column of width w; branch
 // free (surplus loads repeat the last address), all issued before any use.
@@ -127,6 +138,15 @@ __device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const in
 // XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
 // §Workgroup dispatch), so consecutive buckets — which share tile-offset
 // cache lines — are given to blocks of one XCD.  Speed only, never correctness.
+// Tile order for streaming passes: XCD x (blocks b with b % 8 == x) takes
+// the contiguous tile range [x * n/8, (x+1) * n/8), so the lines of a
+// bucket-major per-tile table that 64 consecutive tiles write stay in one
+// XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_tile(int bid, int n) {
+  if (n < 8 || (n & 7)) return bid;
+  return (bid & 7) * (n >> 3) + (bid >> 3);
+}
+
 __device__ __forceinline__ int xcd_bucket(int bid, int nb) {
   if (nb < 8 || (nb & 7)) return bid;
   return (bid & 7) * (nb >> 3) + (bid >> 3);

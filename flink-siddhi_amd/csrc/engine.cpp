@@ -405,7 +405,7 @@ int create_runtime(cep_app* a) {
         const int rw = 1 + std::max(p.nrec_a, p.nrec_b);
         for (int b = 0; b < 2 && ok; ++b)
           ok = dev_ensure(&rt.cf_recs[b], (size_t)cc * rw * 8 + 16, a->stream, false) &&
-               dev_ensure(&rt.cf_toff[b], (size_t)nt * ((1 << lg) + 1) * 2, a->stream, false);
+               dev_ensure(&rt.cf_toff[b], (size_t)nt * ((1 << lg) + 1) * 2 + 16, a->stream, false);
         if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
         rt.cf = true;
         rt.cf_chunk = cc;
@@ -530,12 +530,18 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     CfPartArgs pa{};
     pa.rows = rows;
     pa.pref = rt.pref;
+    pa.ts_slot = -1;
+    for (int i = 0; i < rt.pref.n; ++i)
+      if (rows.cols.p[rt.pref.col[i]] == (const void*)rows.ts && rows.cols.t[rt.pref.col[i]] == T_LONG)
+        pa.ts_slot = i;
     pa.pat = rt.pa;
     pa.cf = cf;
     pa.chunk_base = (int64_t*)rt.chunk_base[b].p;
     pa.recs = (uint64_t*)rt.cf_recs[b].p;
     pa.tile_off = (uint16_t*)rt.cf_toff[b].p;
+    pa.ntiles = (int32_t)ntiles;
     pa.err = (unsigned int*)a->err.p;
+    if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
     if (rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
     {
       LaunchTimer t(a, CEP_K_CF_PARTITION, side);
@@ -555,6 +561,10 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     wa.kstride = rt.kstride;
     wa.out = out_args(o, q);
     wa.err = pa.err;
+    if (a->stamps.p) {
+      wa.stamps = (uint64_t*)a->stamps.p;
+      hipMemsetAsync(wa.stamps, 0, (size_t)4096 * 16 * 8, a->stream);
+    }
     {
       LaunchTimer t(a, CEP_K_CF_WALK);
       launch_cf_walk(wa, P, a->stream);
@@ -772,23 +782,42 @@ void cep_destroy(cep_app* a) {
     const int nb = 1 << a->pats[0].pa.buckets_log2;
     std::vector<uint64_t> st((size_t)nb * 16);
     hipMemcpy(st.data(), a->stamps.p, st.size() * 8, hipMemcpyDeviceToHost);
+    // phases 1..7 of window 0, then phases 2..7 of window 1 (stamps 10..15,
+    // relative to window 0's last stamp); blocks with one window have zeros
     double sum[16] = {0};
-    for (int b = 0; b < nb; ++b)
+    int n1 = 0;
+    for (int b = 0; b < nb; ++b) {
+      const uint64_t* t = &st[(size_t)b * 16];
       for (int i = 1; i < 8; ++i)
-        if (st[b * 16 + i] && st[b * 16 + i - 1]) sum[i] += (double)(st[b * 16 + i] - st[b * 16 + i - 1]);
-    std::fprintf(stderr, "[cep stamps] k_walk phase ticks/block:");
+        if (t[i] && t[i - 1]) sum[i] += (double)(t[i] - t[i - 1]);
+      if (t[10] && t[7]) {
+        ++n1;
+        sum[10] += (double)(t[10] - t[7]);
+        for (int i = 11; i < 16; ++i)
+          if (t[i] && t[i - 1]) sum[i] += (double)(t[i] - t[i - 1]);
+      }
+    }
+    std::fprintf(stderr, "[cep stamps] walk window0 ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);
+    std::fprintf(stderr, "\n[cep stamps] walk window1 (%d blocks):", n1);
+    for (int i = 10; i < 16; ++i) std::fprintf(stderr, " p%d=%.0f", i - 8, n1 ? sum[i] / n1 : 0.0);
     std::fprintf(stderr, "\n");
-    const int nt = (int)std::min<int64_t>(4096, a->pats[0].chunk / (kPartThreads * kPartItems));
+    const bool cf = a->pats[0].cf;
+    const int nt = (int)std::min<int64_t>(4096, cf ? a->pats[0].cf_chunk / kCfTile
+                                                   : a->pats[0].chunk / (kPartThreads * kPartItems));
     std::vector<uint64_t> pt((size_t)nt * 16);
     hipMemcpy(pt.data(), (uint64_t*)a->stamps.p + 4096 * 16, pt.size() * 8, hipMemcpyDeviceToHost);
     double ps[16] = {0};
-    for (int b = 0; b < nt; ++b)
+    uint64_t plo = UINT64_MAX, phi = 0;
+    for (int b = 0; b < nt; ++b) {
       for (int i = 1; i < 8; ++i)
         if (pt[b * 16 + i] && pt[b * 16 + i - 1]) ps[i] += (double)(pt[b * 16 + i] - pt[b * 16 + i - 1]);
-    std::fprintf(stderr, "[cep stamps] k_partition phase ticks/block:");
+      if (pt[b * 16]) plo = std::min(plo, pt[b * 16]);
+      for (int i = 0; i < 8; ++i) phi = std::max(phi, pt[b * 16 + i]);
+    }
+    std::fprintf(stderr, "[cep stamps] partition phase ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, ps[i] / nt);
-    std::fprintf(stderr, "\n");
+    std::fprintf(stderr, " span=%.0f\n", (double)(phi - plo));
   }
   harvest_timers(a);
   for (auto e : a->event_pool) hipEventDestroy(e);

@@ -188,13 +188,13 @@ struct WalkArgs {
 //   w1.. = physical carried words (A rows: A's, B rows: B's)
 // A carried column whose buffer IS the event-ts buffer is not carried: its
 // value is the record's ts (cap_phys / bcol_phys = -1).
-constexpr int kCfPartThreads = 1024;
+constexpr int kCfPartThreads = 512;
 constexpr int kCfItems = 8;                            // rows per lane
-constexpr int kCfTile = kCfPartThreads * kCfItems;     // 8192 rows per tile
-constexpr int kCfWalkThreads = 1024;
-constexpr int kCfWindow = 4096;                        // records per LDS window (nw <= 1)
+constexpr int kCfTile = kCfPartThreads * kCfItems;     // 4096 rows per tile
+constexpr int kCfWalkThreads = 512;
+constexpr int kCfWindow = 2048;                        // records per LDS window (nw <= 1)
 constexpr int kCfMaxKeys = 512;                        // keys per bucket
-constexpr int kCfMaxTiles = 2048;                      // chunk <= 16 Mi rows
+constexpr int kCfMaxTiles = 4096;                      // chunk <= 16 Mi rows
 constexpr int kCfMaxBuckets = 4096;
 constexpr int kCfMaxCaps = 2;                          // captured words per pending slot
 
@@ -208,11 +208,14 @@ struct CfPlan {
 struct CfPartArgs {
   RowsArgs rows;
   PrefPlan pref;
+  int32_t ts_slot;             // prefetch slot whose column IS the event-ts buffer (-1: none)
   PatternArgs pat;
   CfPlan cf;
   int64_t* chunk_base;         // out: {ts, seq} of the chunk's first row
   uint64_t* recs;              // out: records, tile t at recs + t * kCfTile * (1 + nw)
-  uint16_t* tile_off;          // out: [ntiles][P+1] exclusive bucket offsets per tile
+  uint16_t* tile_off;          // out: [P+1][ntiles] exclusive bucket offsets, bucket-major
+  int32_t ntiles;
+  uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per tile 16 s_memtime stamps
   unsigned int* err;
 };
 

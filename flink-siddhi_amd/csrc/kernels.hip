@@ -476,12 +476,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
         if (p.nfa_mode) role = nrole[e];
       }
       if (!role) continue;
-      if (key[e] < 0 || (key[e] % p.key_stride) != p.key_offset) {
-        set_err(a.err, ERR_KEY_RANGE);
-        continue;
-      }
-      const int64_t kfield = key[e] / p.key_stride;
-      if (kfield >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
+      const int64_t kfield = shard_key(key[e], p.key_stride, p.key_offset);
+      if (kfield < 0 || kfield >= p.key_capacity) { set_err(a.err, ERR_KEY_RANGE); continue; }
       const int bucket = (int)(kfield & (P - 1));
       key[e] = kfield;
       const uint32_t rank = atomicAdd(&hist[bucket], 1u);

@@ -14,7 +14,7 @@ import sys
 
 
 def short(name):
-    for k in ("k_partition", "k_walk", "k_filter", "k_generate"):
+    for k in ("k_cfpart", "k_cfwalk", "k_partition", "k_walk", "k_filter", "k_generate", "k_route"):
         if k in name:
             return k
     return None
