@@ -37,7 +37,7 @@ namespace cep {
 namespace {
 
 constexpr uint16_t kNoB = 0xffff;
-constexpr int kCfStageBytes = 36 * 1024;    // a tile keeps ~1/3 of its rows at config 3
+constexpr int kCfStageBytes = (kCfTile / 8192 * 20 + 36) * 1024;    // a tile keeps ~1/3 of its rows at config 3
 
 // Block-wide exclusive scan of one value per thread, NT <= 1024 threads;
 // scratch holds NT / 64 + 1 words.
@@ -86,7 +86,7 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 
 // ============================================================== k_cfpart ==
 template <int NW>
-__global__ __launch_bounds__(kCfPartThreads, 4) void k_cfpart(CfPartArgs a) {   // 2 workgroups per CU
+__global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
   __shared__ uint32_t scratch[NT / 64 + 1];
@@ -371,7 +371,16 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   // loaded now so the state read overlaps the gather below
   const bool klane = tid < kpb;
   const int64_t kidx = (int64_t)bucket * kpb + tid;
-  uint64_t* ksl = a.kslot + kidx;   // slot j word w: ksl[(j * sw + w) * ks]
+  // slot j word w of this key at byte kb + (j * sw + w) * pb of kslot: 32-bit
+  // offsets from the kernel-argument base (the host checks the state fits
+  // 4 GiB) keep no 64-bit per-slot addresses live in registers
+  const uint32_t kb = (uint32_t)kidx * 8u, pb = (uint32_t)ks * 8u;
+  auto sl_ld = [&](int j, int w) -> uint64_t {
+    return *(const uint64_t*)((const char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb));
+  };
+  auto sl_st = [&](int j, int w, uint64_t v) {
+    *(uint64_t*)((char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb)) = v;
+  };
   uint32_t hdr = klane ? a.khdr[kidx] : 0u;
   int n = (int)(hdr & 0xffu);
   // Slots 0 / 1 (ts + captures) live in registers for the whole kernel: read
@@ -382,18 +391,18 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   const bool c1 = sw > 2, c2 = sw > 3;
   uint64_t t0r = 0, t1r = 0, a0c0 = 0, a0c1 = 0, a1c0 = 0, a1c1 = 0;
   if (n > 0) {
-    t0r = ksl[0];
-    if (c1) a0c0 = ksl[2 * ks];
-    if (c2) a0c1 = ksl[3 * ks];
+    t0r = sl_ld(0, 0);
+    if (c1) a0c0 = sl_ld(0, 2);
+    if (c2) a0c1 = sl_ld(0, 3);
   }
   if (n > 1) {
-    t1r = ksl[(int64_t)sw * ks];
-    if (c1) a1c0 = ksl[(int64_t)(sw + 2) * ks];
-    if (c2) a1c1 = ksl[(int64_t)(sw + 3) * ks];
+    t1r = sl_ld(1, 0);
+    if (c1) a1c0 = sl_ld(1, 2);
+    if (c2) a1c1 = sl_ld(1, 3);
   }
   // (masked selects: a select chain on j / w is turned into a stack array)
   auto slot_word = [&](int j, int w) -> uint64_t {
-    if (j >= 2) return ksl[((int64_t)j * sw + w) * ks];
+    if (j >= 2) return sl_ld(j, w);
     const uint64_t m0 = 0ull - (uint64_t)(j == 0), m1 = ~m0;
     const uint64_t w0 = 0ull - (uint64_t)(w == 0), w2 = 0ull - (uint64_t)(w == 2);
     const uint64_t w3 = 0ull - (uint64_t)(w == 3);
@@ -414,10 +423,18 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
     const uint16_t* rhi = rlo + ntiles;
     const int tb = tid * TPT;
-    if ((ntiles & 7) == 0 && tb + TPT <= ntiles) {
-      const uint4 x = gload4(rlo + tb), y = gload4(rhi + tb);
-      lop[0] = x.x; lop[1] = x.y; lop[2] = x.z; lop[3] = x.w;
-      const uint32_t ys[4] = {y.x, y.y, y.z, y.w};
+    if ((ntiles & (TPT - 1)) == 0 && tb + TPT <= ntiles) {
+      // TPT u16 per row: one 8- or 16-byte load per row
+      uint32_t ys[TPT / 2];
+      if constexpr (TPT == 8) {
+        const uint4 x = *(const uint4*)(rlo + tb), y = *(const uint4*)(rhi + tb);
+        lop[0] = x.x; lop[1 % (TPT / 2)] = x.y; lop[2 % (TPT / 2)] = x.z; lop[3 % (TPT / 2)] = x.w;
+        ys[0] = y.x; ys[1 % (TPT / 2)] = y.y; ys[2 % (TPT / 2)] = y.z; ys[3 % (TPT / 2)] = y.w;
+      } else {
+        const uint2 x = *(const uint2*)(rlo + tb), y = *(const uint2*)(rhi + tb);
+        lop[0] = x.x; lop[1 % (TPT / 2)] = x.y;
+        ys[0] = y.x; ys[1 % (TPT / 2)] = y.y;
+      }
 #pragma unroll
       for (int i = 0; i < TPT; ++i)
         cnt[i] = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
@@ -754,10 +771,9 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         t1r = (ts & m1) | (t1r & ~m1);
         a1c0 = (x0 & m1) | (a1c0 & ~m1);
         a1c1 = (x1 & m1) | (a1c1 & ~m1);
-        uint64_t* dst = ksl + (int64_t)nn * sw * ks;
-        dst[0] = ts;
-        if (c1) dst[2 * ks] = x0;
-        if (c2) dst[3 * ks] = x1;
+        sl_st(nn, 0, ts);
+        if (c1) sl_st(nn, 2, x0);
+        if (c2) sl_st(nn, 3, x1);
         ++nn;
       };
       if (lb == kNoB) {

@@ -393,7 +393,8 @@ int create_runtime(cep_app* a) {
     {
       bool ok = p.closed_form && !q.nfa && !agg && !rt.part_vm && !rt.walk_vm && rt.pref.n >= 0 &&
                 p.ncap <= kCfMaxCaps && p.nrec_a <= kPfRec && p.nrec_b <= kPfRec &&
-                kpb <= kCfMaxKeys && (1 << lg) <= kCfMaxBuckets && !std::getenv("CEP_NO_CF");
+                kpb <= kCfMaxKeys && (1 << lg) <= kCfMaxBuckets && !std::getenv("CEP_NO_CF") &&
+                (double)rt.kstride * S * p.slot_words * 8 < 4294967296.0;   // 32-bit slot offsets
       for (auto& it : q.select)
         ok = ok && (it.src == SRC_KEY || (it.src >= SRC_CAP && it.src < SRC_CAP + kCfMaxCaps) ||
                     (it.src >= SRC_REC && it.src < SRC_REC + kPfRec));
@@ -561,6 +562,8 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     wa.kstride = rt.kstride;
     wa.out = out_args(o, q);
     wa.err = pa.err;
+    static const int ablate = std::getenv("CEP_ABLATE") ? std::atoi(std::getenv("CEP_ABLATE")) : 0;
+    wa.ablate = ablate;
     if (a->stamps.p) {
       wa.stamps = (uint64_t*)a->stamps.p;
       hipMemsetAsync(wa.stamps, 0, (size_t)4096 * 16 * 8, a->stream);

@@ -188,13 +188,16 @@ struct WalkArgs {
 //   w1.. = physical carried words (A rows: A's, B rows: B's)
 // A carried column whose buffer IS the event-ts buffer is not carried: its
 // value is the record's ts (cap_phys / bcol_phys = -1).
-constexpr int kCfPartThreads = 512;
+#ifndef CF_TILE_ROWS
+#define CF_TILE_ROWS 8192
+#endif
 constexpr int kCfItems = 8;                            // rows per lane
-constexpr int kCfTile = kCfPartThreads * kCfItems;     // 4096 rows per tile
+constexpr int kCfPartThreads = CF_TILE_ROWS / kCfItems;   // 512 (2 workgroups per CU) or 1024
+constexpr int kCfTile = CF_TILE_ROWS;                  // rows per tile
 constexpr int kCfWalkThreads = 512;
 constexpr int kCfWindow = 2048;                        // records per LDS window (nw <= 1)
 constexpr int kCfMaxKeys = 512;                        // keys per bucket
-constexpr int kCfMaxTiles = 4096;                      // chunk <= 16 Mi rows
+constexpr int kCfMaxTiles = (16 << 20) / kCfTile;      // chunk <= 16 Mi rows
 constexpr int kCfMaxBuckets = 4096;
 constexpr int kCfMaxCaps = 2;                          // captured words per pending slot
 
@@ -231,6 +234,7 @@ struct CfWalkArgs {
   int64_t kstride;
   OutArgs out;
   uint64_t* stamps;
+  int32_t ablate;              // diagnostics (CEP_ABLATE): bit 0 no emission, 1 no commit, 2 no rank/reload
   unsigned int* err;
 };
 
