@@ -85,7 +85,7 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 }  // namespace
 
 // ============================================================== k_cfpart ==
-template <int NW>
+template <int NW, bool FR>   // FR: rows are received shuffle records
 __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
@@ -100,10 +100,10 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   CF_STAMP(0);
   for (int i = tid; i <= P; i += NT) hist[i] = 0;
 
-  const int64_t ts_base = a.rows.ts[a.rows.row0];
+  const int64_t ts_base = FR ? (int64_t)a.in_recs[a.rows.row0 * a.in_rec_words + 2] : a.rows.ts[a.rows.row0];
   if (tile == 0 && tid == 0) {
     a.chunk_base[0] = ts_base;
-    a.chunk_base[1] = a.rows.seq0 + a.rows.row0;
+    a.chunk_base[1] = FR ? (int64_t)a.in_recs[a.rows.row0 * a.in_rec_words + 1] : a.rows.seq0 + a.rows.row0;
   }
   // Lane-interleaved rows: lane l of wave w owns rows w*64*E + 64*e + l
   // (e < E), so every load instruction reads one contiguous 64-row segment
@@ -119,7 +119,42 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   uint64_t pv[kPref][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) tsv[e] = 0;
-  if (valid) {
+  uint64_t fkey[FR ? E : 1], fc0[FR ? E : 1], fc1[FR ? E : 1];
+  if (FR && valid) {
+    // received records: roles and keys were computed by the sender (k_route)
+    const int rw = a.in_rec_words;
+    uint64_t hv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const bool ok = (valid >> e) & 1u;
+      const uint64_t* r = a.in_recs + (row0 + 64 * e) * rw;
+      hv[e] = ok ? r[0] : 0ull;
+      tsv[e] = ok ? r[2] : 0ull;
+      const bool isa = ((hv[e] >> 32) & ROLE_A) != 0;
+      fc0[e] = (ok && NW > 0) ? r[3 + (isa ? a.cf.a_log[0] : a.cf.b_log[0])] : 0ull;
+      fc1[e] = (ok && NW > 1) ? r[3 + (isa ? a.cf.a_log[1] : a.cf.b_log[1])] : 0ull;
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t role = (uint32_t)(hv[e] >> 32) & 0xffu;
+      role_a |= ((role & ROLE_A) ? 1u : 0u) << e;
+      role_b |= ((role & ROLE_B) && (role & ROLE_G) ? 1u : 0u) << e;
+      fkey[e] = (uint64_t)(uint32_t)hv[e];
+    }
+    if (p.within >= 0) {
+      const int64_t before = row0 > 0 ? (int64_t)a.in_recs[(row0 - 1) * rw + 2] : a.rows.prev_ts;
+      bool bad = false;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const uint64_t up = __shfl_up(tsv[e], 1, 64);
+        const uint64_t last = e > 0 ? __shfl(tsv[e > 0 ? e - 1 : 0], 63, 64) : 0ull;
+        const int64_t prev = lane > 0 ? (int64_t)up : (e > 0 ? (int64_t)last : before);
+        if ((valid >> e) & 1u) bad |= (int64_t)tsv[e] < prev;
+      }
+      if (bad) set_err(a.err, ERR_ORDER);
+    }
+  }
+  if (!FR && valid) {
     // every load of the lane's rows is issued before any use; unused slots
     // and the ts alias issue none (uniform branches)
     uint32_t sb[E];
@@ -199,7 +234,9 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     lkey[e] = 0;
     const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B;
     if (!role) continue;
-    const int64_t key = a.pref.key_slot >= 0 ? (int64_t)pick<E>(pv, a.pref.key_slot, e) : 0;
+    int64_t key;
+    if constexpr (FR) key = (int64_t)fkey[e];
+    else key = a.pref.key_slot >= 0 ? (int64_t)pick<E>(pv, a.pref.key_slot, e) : 0;
     const int64_t kfield = shard_key(key, p.key_stride, p.key_offset);
     if (kfield < 0 || kfield >= p.key_capacity) {
       set_err(a.err, ERR_KEY_RANGE);
@@ -253,8 +290,13 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
                         ((uint64_t)role << 45) | ((uint64_t)lkey[e] << 48);
     const bool isa = (role & ROLE_A) != 0;
     uint64_t c0 = 0, c1 = 0;
-    if (NW > 0) c0 = pick<E>(pv, isa ? a.cf.a_slot[0] : a.cf.b_slot[0], e);
-    if (NW > 1) c1 = pick<E>(pv, isa ? a.cf.a_slot[1] : a.cf.b_slot[1], e);
+    if constexpr (FR) {
+      c0 = fc0[e];
+      c1 = fc1[e];
+    } else {
+      if (NW > 0) c0 = pick<E>(pv, isa ? a.cf.a_slot[0] : a.cf.b_slot[0], e);
+      if (NW > 1) c1 = pick<E>(pv, isa ? a.cf.a_slot[1] : a.cf.b_slot[1], e);
+    }
     // explicit address spaces (a generic pointer would make these flat stores)
     if (staged) {
       stage[slot * RW] = w0;
@@ -382,6 +424,37 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     *(uint64_t*)((char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb)) = v;
   };
   uint32_t hdr = klane ? a.khdr[kidx] : 0u;
+
+  // ---- the bucket's segment in every tile: two contiguous rows of the
+  // bucket-major offset table, loaded before the slot loads below (those
+  // wait for hdr; these need not)
+  const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
+  const uint16_t* rhi = rlo + ntiles;
+  const int tb = tid * TPT;
+  uint32_t lop[TPT / 2];   // packed u16 segment starts of tiles tid*TPT + i
+  uint32_t ys[TPT / 2];    // packed u16 segment ends
+  if ((ntiles & (TPT - 1)) == 0 && tb + TPT <= ntiles) {
+    // TPT u16 per row: one 8- or 16-byte load per row
+    if constexpr (TPT == 8) {
+      const uint4 x = *(const uint4*)(rlo + tb), y = *(const uint4*)(rhi + tb);
+      lop[0] = x.x; lop[1 % (TPT / 2)] = x.y; lop[2 % (TPT / 2)] = x.z; lop[3 % (TPT / 2)] = x.w;
+      ys[0] = y.x; ys[1 % (TPT / 2)] = y.y; ys[2 % (TPT / 2)] = y.z; ys[3 % (TPT / 2)] = y.w;
+    } else {
+      const uint2 x = *(const uint2*)(rlo + tb), y = *(const uint2*)(rhi + tb);
+      lop[0] = x.x; lop[1 % (TPT / 2)] = x.y;
+      ys[0] = y.x; ys[1 % (TPT / 2)] = y.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TPT / 2; ++i) lop[i] = ys[i] = 0;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      const int t = tb + i;
+      lop[i >> 1] |= (t < ntiles ? (uint32_t)rlo[t] : 0u) << (16 * (i & 1));
+      ys[i >> 1] |= (t < ntiles ? (uint32_t)rhi[t] : 0u) << (16 * (i & 1));
+    }
+  }
+
   int n = (int)(hdr & 0xffu);
   // Slots 0 / 1 (ts + captures) live in registers for the whole kernel: read
   // once here, rewritten by the commit of each window (named scalars: a
@@ -413,42 +486,14 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   const int64_t seq_base = a.chunk_base[1];
   for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
 
-  // ---- the bucket's segment in every tile (two contiguous rows of the
-  // bucket-major offset table) -> exclusive prefix over tiles; this thread's
-  // segment starts stay in registers for the gather
-  uint32_t lop[TPT / 2];   // packed u16 segment starts of tiles tid*TPT + i
+  // ---- segment sizes -> exclusive prefix over tiles; this thread's segment
+  // starts stay in registers (lop) for the gather
   {
     uint32_t cnt[TPT];
     uint32_t sum = 0;
-    const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
-    const uint16_t* rhi = rlo + ntiles;
-    const int tb = tid * TPT;
-    if ((ntiles & (TPT - 1)) == 0 && tb + TPT <= ntiles) {
-      // TPT u16 per row: one 8- or 16-byte load per row
-      uint32_t ys[TPT / 2];
-      if constexpr (TPT == 8) {
-        const uint4 x = *(const uint4*)(rlo + tb), y = *(const uint4*)(rhi + tb);
-        lop[0] = x.x; lop[1 % (TPT / 2)] = x.y; lop[2 % (TPT / 2)] = x.z; lop[3 % (TPT / 2)] = x.w;
-        ys[0] = y.x; ys[1 % (TPT / 2)] = y.y; ys[2 % (TPT / 2)] = y.z; ys[3 % (TPT / 2)] = y.w;
-      } else {
-        const uint2 x = *(const uint2*)(rlo + tb), y = *(const uint2*)(rhi + tb);
-        lop[0] = x.x; lop[1 % (TPT / 2)] = x.y;
-        ys[0] = y.x; ys[1 % (TPT / 2)] = y.y;
-      }
 #pragma unroll
-      for (int i = 0; i < TPT; ++i)
-        cnt[i] = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
-    } else {
-#pragma unroll
-      for (int i = 0; i < TPT / 2; ++i) lop[i] = 0;
-#pragma unroll
-      for (int i = 0; i < TPT; ++i) {
-        const int t = tb + i;
-        const uint32_t lo = t < ntiles ? rlo[t] : 0u;
-        lop[i >> 1] |= lo << (16 * (i & 1));
-        cnt[i] = t < ntiles ? (uint32_t)rhi[t] - lo : 0u;
-      }
-    }
+    for (int i = 0; i < TPT; ++i)
+      cnt[i] = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
 #pragma unroll
     for (int i = 0; i < TPT; ++i) sum += cnt[i];
     uint32_t total;
@@ -613,6 +658,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         const uint64_t w0 = ((uint64_t)x[i].y << 32) | x[i].x;
         L.sts[s] = x[i].x;
         L.sseq[s] = (gr[i] & ~(uint32_t)(kCfTile - 1)) + rec_row(w0);
+        if (a.in_seq)   // received records: global arrival number - chunk base
+          L.sseq[s] = (uint32_t)((int64_t)a.in_seq[(int64_t)L.sseq[s] * a.in_rec_words] - seq_base);
         L.skr[s] = (uint16_t)(rec_key(w0) | (rec_role(w0) << 12));
         if (NW > 0) L.scap[0][s] = ((uint64_t)x[i].w << 32) | x[i].z;
         if (NW > 1) L.scap[NW > 1 ? 1 : 0][s] = y[i];
@@ -715,33 +762,12 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     lds_barrier();
     CF_STAMP(wi * 8 + 5);
     const unsigned long long base = L.base;
-
-    // ---- emit record matches (lane per sorted position; LDS reads + stores)
     const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
-#pragma unroll 1
-    for (int i = 0; i < PER; ++i) {
-      const uint32_t q = tid + i * NT;
-      if (q >= nw) continue;
-      const uint32_t kr = L.skr[q];
-      const uint16_t nb = L.nextb[q];
-      if (!((kr >> 12) & ROLE_A) || nb == kNoB) continue;
-      const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
-      if (W >= 0 && (d < 0 ? -d : d) > W) continue;
-      const uint32_t k = kr & 0xfffu;
-      const uint32_t extra = q == L.kstart[k] ? L.cm[k] : 0u;
-      const int64_t ats = ts_base + (int64_t)L.sts[q];
-      const int64_t bts = ts_base + (int64_t)L.sts[nb];
-      const uint64_t a0 = NW > 0 ? L.scap[0][q] : 0ull, a1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][q] : 0ull;
-      const uint64_t x0 = cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1);
-      const uint64_t x1 = cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1);
-      const int64_t kl = ((int64_t)k << lg) | bucket;
-      cf_emit(a, base + L.v[q] + extra, kl * p.key_stride + p.key_offset, x0, x1,
-              NW > 0 ? L.scap[0][nb] : 0ull, NW > 1 ? L.scap[NW > 1 ? 1 : 0][nb] : 0ull, bts,
-              seq_base + (int64_t)L.sseq[nb]);
-    }
-    CF_STAMP(wi * 8 + 6);
 
-    // ---- key lanes: carried matches, survivors, state commit
+    // ---- key lanes: carried matches, survivors, state commit.  Runs before
+    // the record emission: a slot read (slots >= 2 live in HBM) issued after
+    // a wave's output stores waits for all of them (vmcnt counts loads and
+    // stores in issue order), so the state work goes first.
     if (klane && r1 > r0) {
       const int64_t kl = ((int64_t)tid << lg) | bucket;
       const int64_t kv = kl * p.key_stride + p.key_offset;
@@ -807,6 +833,30 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       hdr = (hdr & ~0xffu) | (uint32_t)nn;
       a.khdr[kidx] = hdr;
     }
+    CF_STAMP(wi * 8 + 6);
+
+    // ---- emit record matches (lane per sorted position; LDS reads + stores)
+#pragma unroll 1
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t q = tid + i * NT;
+      if (q >= nw) continue;
+      const uint32_t kr = L.skr[q];
+      const uint16_t nb = L.nextb[q];
+      if (!((kr >> 12) & ROLE_A) || nb == kNoB) continue;
+      const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
+      if (W >= 0 && (d < 0 ? -d : d) > W) continue;
+      const uint32_t k = kr & 0xfffu;
+      const uint32_t extra = q == L.kstart[k] ? L.cm[k] : 0u;
+      const int64_t ats = ts_base + (int64_t)L.sts[q];
+      const int64_t bts = ts_base + (int64_t)L.sts[nb];
+      const uint64_t a0 = NW > 0 ? L.scap[0][q] : 0ull, a1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][q] : 0ull;
+      const uint64_t x0 = cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1);
+      const uint64_t x1 = cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1);
+      const int64_t kl = ((int64_t)k << lg) | bucket;
+      cf_emit(a, base + L.v[q] + extra, kl * p.key_stride + p.key_offset, x0, x1,
+              NW > 0 ? L.scap[0][nb] : 0ull, NW > 1 ? L.scap[NW > 1 ? 1 : 0][nb] : 0ull, bts,
+              seq_base + (int64_t)L.sseq[nb]);
+    }
     CF_STAMP(wi * 8 + 7);
     if (over) {
       piece += nw;
@@ -830,10 +880,19 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
   const int P = 1 << a.pat.buckets_log2;
   const size_t dyn = ((size_t)(P + 1) * 4 + 15) & ~(size_t)15;
+  const dim3 g((unsigned)ntiles), b(kCfPartThreads);
+  if (a.in_recs) {
+    switch (a.cf.nw) {
+      case 0: hipLaunchKernelGGL((k_cfpart<0, true>), g, b, dyn, s, a); break;
+      case 1: hipLaunchKernelGGL((k_cfpart<1, true>), g, b, dyn, s, a); break;
+      default: hipLaunchKernelGGL((k_cfpart<2, true>), g, b, dyn, s, a); break;
+    }
+    return;
+  }
   switch (a.cf.nw) {
-    case 0: hipLaunchKernelGGL(k_cfpart<0>, dim3((unsigned)ntiles), dim3(kCfPartThreads), dyn, s, a); break;
-    case 1: hipLaunchKernelGGL(k_cfpart<1>, dim3((unsigned)ntiles), dim3(kCfPartThreads), dyn, s, a); break;
-    default: hipLaunchKernelGGL(k_cfpart<2>, dim3((unsigned)ntiles), dim3(kCfPartThreads), dyn, s, a); break;
+    case 0: hipLaunchKernelGGL((k_cfpart<0, false>), g, b, dyn, s, a); break;
+    case 1: hipLaunchKernelGGL((k_cfpart<1, false>), g, b, dyn, s, a); break;
+    default: hipLaunchKernelGGL((k_cfpart<2, false>), g, b, dyn, s, a); break;
   }
 }
 

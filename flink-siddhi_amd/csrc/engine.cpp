@@ -486,21 +486,27 @@ bool pref_aligned(const PrefPlan& pf, const RowsArgs& rows) {
 
 // Per-batch layout of the closed-form fast path's records: carried columns
 // whose buffer is the batch's event-ts buffer are rebuilt from the record ts.
-bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf) {
+bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf, bool from_records = false) {
   const PatternArgs& p = rt.pa;
   std::memset(cf, 0, sizeof(*cf));
   int a_phys[kMaxCaps], b_phys[kMaxCaps];
   int na = 0, nb = 0;
   auto alias = [&](int col) {
-    return rows.cols.p[col] == (const void*)rows.ts && rows.cols.t[col] == T_LONG;
+    return !from_records && rows.cols.p[col] == (const void*)rows.ts && rows.cols.t[col] == T_LONG;
   };
   for (int c = 0; c < p.nrec_a; ++c) {
     a_phys[c] = alias(p.rec_a[c]) ? -1 : na;
-    if (a_phys[c] >= 0) cf->a_slot[na++] = rt.pref.reca_slot[c];
+    if (a_phys[c] >= 0) {
+      cf->a_log[na] = c;
+      cf->a_slot[na++] = rt.pref.reca_slot[c];
+    }
   }
   for (int c = 0; c < p.nrec_b; ++c) {
     b_phys[c] = alias(p.rec_b[c]) ? -1 : nb;
-    if (b_phys[c] >= 0) cf->b_slot[nb++] = rt.pref.recb_slot[c];
+    if (b_phys[c] >= 0) {
+      cf->b_log[nb] = c;
+      cf->b_slot[nb++] = rt.pref.recb_slot[c];
+    }
   }
   cf->nw = std::max(na, nb);
   if (cf->nw > 2) return false;
@@ -514,7 +520,8 @@ bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf) {
 // Closed-form fast path: k_cfpart(c+1) on the side stream overlaps
 // k_cfwalk(c) on the main stream (double-buffered arenas).
 int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
-                   const RowsArgs& rows_all, const CfPlan& cf) {
+                   const RowsArgs& rows_all, const CfPlan& cf,
+                   const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
   const int P = 1 << rt.pa.buckets_log2;
   hipEventRecord(a->in_ready, a->stream);
   hipStreamWaitEvent(a->side, a->in_ready, 0);
@@ -532,7 +539,9 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     pa.rows = rows;
     pa.pref = rt.pref;
     pa.ts_slot = -1;
-    for (int i = 0; i < rt.pref.n; ++i)
+    pa.in_recs = in_recs;
+    pa.in_rec_words = in_rec_words;
+    for (int i = 0; i < rt.pref.n && !in_recs; ++i)
       if (rows.cols.p[rt.pref.col[i]] == (const void*)rows.ts && rows.cols.t[rt.pref.col[i]] == T_LONG)
         pa.ts_slot = i;
     pa.pat = rt.pa;
@@ -562,6 +571,8 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     wa.kstride = rt.kstride;
     wa.out = out_args(o, q);
     wa.err = pa.err;
+    wa.in_seq = in_recs ? in_recs + rows.row0 * in_rec_words + 1 : nullptr;
+    wa.in_rec_words = in_rec_words;
     static const int ablate = std::getenv("CEP_ABLATE") ? std::atoi(std::getenv("CEP_ABLATE")) : 0;
     wa.ablate = ablate;
     if (a->stamps.p) {
@@ -586,9 +597,10 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
   o.bound += rows_all.n;
   int rc = ensure_out_cap(a, o, o.bound);
   if (rc) return rc;
-  if (rt.cf && !in_recs && pref_aligned(rt.pref, rows_all)) {
+  if (rt.cf && (in_recs || pref_aligned(rt.pref, rows_all))) {
     CfPlan cf;
-    if (cf_plan(rt, rows_all, &cf)) return run_pattern_cf(a, rt, q, o, rows_all, cf);
+    if (cf_plan(rt, rows_all, &cf, in_recs != nullptr))
+      return run_pattern_cf(a, rt, q, o, rows_all, cf, in_recs, in_rec_words);
   }
   const int P = 1 << rt.pa.buckets_log2;
   // the side stream starts after everything already queued on the main stream

@@ -204,6 +204,7 @@ constexpr int kCfMaxCaps = 2;                          // captured words per pen
 struct CfPlan {
   int32_t nw;                      // physical carried words per record (0..2)
   int32_t a_slot[2], b_slot[2];    // prefetch slot of physical word w (A rows / B rows)
+  int32_t a_log[2], b_log[2];      // received records: logical carried word of physical word w
   int32_t cap_phys[kMaxCaps];      // A capture i -> physical word, -1 = the A's event ts
   int32_t bcol_phys[kMaxCaps];     // B record word c (SRC_REC + c) -> physical word, -1 = ts
 };
@@ -212,6 +213,10 @@ struct CfPartArgs {
   RowsArgs rows;
   PrefPlan pref;
   int32_t ts_slot;             // prefetch slot whose column IS the event-ts buffer (-1: none)
+  // received shuffle records (cep_send_records): rows are wide records
+  // [hdr = key | role << 32 | stream << 40, global seq, ts, logical carried...]
+  const uint64_t* in_recs;     // nullptr: rows are columns
+  int32_t in_rec_words;
   PatternArgs pat;
   CfPlan cf;
   int64_t* chunk_base;         // out: {ts, seq} of the chunk's first row
@@ -233,6 +238,8 @@ struct CfWalkArgs {
   uint64_t* kslot;
   int64_t kstride;
   OutArgs out;
+  const uint64_t* in_seq;      // received records: &record[row0].seq (global arrival numbers), else nullptr
+  int32_t in_rec_words;
   uint64_t* stamps;
   int32_t ablate;              // diagnostics (CEP_ABLATE): bit 0 no emission, 1 no commit, 2 no rank/reload
   unsigned int* err;

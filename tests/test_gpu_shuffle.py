@@ -8,6 +8,7 @@ import pytest
 import torch
 
 import flink_siddhi as fs
+from flink_siddhi import _lib as L
 from flink_siddhi import workload
 from helpers import assert_same_rows, engine_rows, oracle_run, workload_events
 
@@ -18,8 +19,15 @@ def _dev(w):
     return {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in w.items()}
 
 
+@pytest.mark.parametrize("path", ["cf", "general"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_route_exchange_matches_oracle(world):
+def test_route_exchange_matches_oracle(world, path, monkeypatch):
+    # owners run the received records through the closed-form fast path
+    # (k_cfpart from records) or, with CEP_NO_CF=1, the general k_partition
+    if path == "general":
+        monkeypatch.setenv("CEP_NO_CF", "1")
+    else:
+        monkeypatch.delenv("CEP_NO_CF", raising=False)
     n_per, keys = 12000, 600
     plan = workload.PATTERN_PLAN
     sender = fs.SiddhiAppRuntime(plan)
@@ -44,6 +52,11 @@ def test_route_exchange_matches_oracle(world):
         owners[r].send_records(recv, recv.shape[0], n_per)
         owners[r].flush()
         got += engine_rows(owners[r].collect("O"))
+        st = owners[r].stats()
+        if path == "cf":
+            assert st.kernel_launches[L.K_CF_WALK] > 0 and st.kernel_launches[L.K_WALK] == 0
+        else:
+            assert st.kernel_launches[L.K_CF_WALK] == 0 and st.kernel_launches[L.K_WALK] > 0
     got.sort(key=lambda t: t[1])
     w = workload.generate(0, world * n_per, keys, rate=1)
     want = oracle_run(plan, workload_events(w)).get("O", [])
