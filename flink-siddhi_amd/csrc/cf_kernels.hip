@@ -77,6 +77,31 @@ __device__ __forceinline__ uint32_t bscan(uint32_t v, uint32_t* scratch, uint32_
       a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();      \
   } while (0)
 
+// Diagnostics (CEP_STAMPS=1 CEP_ABLATE=256): event counters of the walk (last launch).
+#define CF_COUNT(i, v)                                                                       \
+  do {                                                                                       \
+    if (a.stamps && (a.ablate & 256))                                                        \
+      atomicAdd((unsigned long long*)&a.stamps[4095 * 16 + (i)], (unsigned long long)(v));   \
+  } while (0)
+
+// Carried word of each row: slot sa on A rows (role_a bit set), sb otherwise;
+// both slots uniform.
+template <int E>
+__device__ __forceinline__ void pick_carried(const uint64_t (&pv)[kPref][E], int sa, int sb,
+                                             uint32_t role_a, uint64_t (&out)[E]) {
+  take_slot<E>(pv, sa, out);
+  if (sb != sa) {
+#pragma unroll
+    for (int q = 0; q < kPref; ++q) {
+      if (sb == q) {
+        asm volatile("");
+#pragma unroll
+        for (int e = 0; e < E; ++e) out[e] = ((role_a >> e) & 1u) ? out[e] : pv[q][e];
+      }
+    }
+  }
+}
+
 // Record field accessors (w0).
 __device__ __forceinline__ uint32_t rec_row(uint64_t w0) { return (uint32_t)(w0 >> 32) & 0x1fffu; }
 __device__ __forceinline__ uint32_t rec_role(uint64_t w0) { return (uint32_t)(w0 >> 45) & 0x7u; }
@@ -119,7 +144,9 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   uint64_t pv[kPref][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) tsv[e] = 0;
-  uint64_t fkey[FR ? E : 1], fc0[FR ? E : 1], fc1[FR ? E : 1];
+  uint64_t fkey[E], fc0[E], fc1[E];   // key and carried words per row
+#pragma unroll
+  for (int e = 0; e < E; ++e) fkey[e] = fc0[e] = fc1[e] = 0;
   if (FR && valid) {
     // received records: roles and keys were computed by the sender (k_route)
     const int rw = a.in_rec_words;
@@ -221,6 +248,14 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     const uint32_t all = (1u << E) - 1u;
     if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
     if (is_b) role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
+    // key (the host puts the key column in slot 0) and carried words (A
+    // rows: the A's columns, else the B's) picked now, so pv dies here
+    if (NW > 0) pick_carried<E>(pv, a.cf.a_slot[0], a.cf.b_slot[0], role_a, fc0);
+    if (NW > 1) pick_carried<E>(pv, a.cf.a_slot[1], a.cf.b_slot[1], role_a, fc1);
+    if (a.pref.key_slot >= 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) fkey[e] = pv[0][e];
+    }
   }
   lds_barrier();   // hist zeroed
   CF_STAMP(1);
@@ -235,8 +270,7 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B;
     if (!role) continue;
     int64_t key;
-    if constexpr (FR) key = (int64_t)fkey[e];
-    else key = a.pref.key_slot >= 0 ? (int64_t)pick<E>(pv, a.pref.key_slot, e) : 0;
+    key = (int64_t)fkey[e];
     const int64_t kfield = shard_key(key, p.key_stride, p.key_offset);
     if (kfield < 0 || kfield >= p.key_capacity) {
       set_err(a.err, ERR_KEY_RANGE);
@@ -288,15 +322,7 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     if (dts < 0 || dts > 0xffffffffll) set_err(a.err, ERR_ORDER);
     const uint64_t w0 = (uint64_t)(uint32_t)dts | ((uint64_t)(wave * 64 * E + 64 * e + lane) << 32) |
                         ((uint64_t)role << 45) | ((uint64_t)lkey[e] << 48);
-    const bool isa = (role & ROLE_A) != 0;
-    uint64_t c0 = 0, c1 = 0;
-    if constexpr (FR) {
-      c0 = fc0[e];
-      c1 = fc1[e];
-    } else {
-      if (NW > 0) c0 = pick<E>(pv, isa ? a.cf.a_slot[0] : a.cf.b_slot[0], e);
-      if (NW > 1) c1 = pick<E>(pv, isa ? a.cf.a_slot[1] : a.cf.b_slot[1], e);
-    }
+    const uint64_t c0 = fc0[e], c1 = fc1[e];
     // explicit address spaces (a generic pointer would make these flat stores)
     if (staged) {
       stage[slot * RW] = w0;
@@ -338,7 +364,11 @@ struct CfWalkLds {
   uint32_t seg[kCfMaxTiles + 1];       // exclusive prefix of the bucket's segment sizes
   uint32_t kstart[kCfMaxKeys + 1];     // key runs (sorted positions)
   uint32_t kcur[kCfMaxKeys];           // counting-sort cursors
-  uint32_t wrec[WIN];                  // arena record index per window slot
+  union {
+    uint32_t wrec[WIN];                // arena record index per window slot (gather, reload)
+    uint64_t pcache[WIN / 2];          // from p4: key lanes' pending slots >= 2 (ts, captures)
+  };
+  uint32_t pc_used;                    // pcache words handed out this window
   union {
     uint64_t kent[WIN];                // seq << 20 | key << 11 | slot, grouped by key
     uint64_t scap[NW > 0 ? NW : 1][WIN];   // sorted: physical carried words
@@ -463,6 +493,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   // written here; slots >= 2 stay in HBM.
   const bool c1 = sw > 2, c2 = sw > 3;
   uint64_t t0r = 0, t1r = 0, a0c0 = 0, a0c1 = 0, a1c0 = 0, a1c1 = 0;
+  bool dirty = false;   // header / slots 0-1 changed: stored at kernel end
   if (n > 0) {
     t0r = sl_ld(0, 0);
     if (c1) a0c0 = sl_ld(0, 2);
@@ -474,8 +505,17 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     if (c2) a1c1 = sl_ld(1, 3);
   }
   // (masked selects: a select chain on j / w is turned into a stack array)
+  // Per window, a key lane copies its slots >= 2 (one batch of independent
+  // loads, before any of the window's stores) to pcache: words pcb + (j - 2)
+  // * cw + {0: ts, 1: capture 0, 2: capture 1} for j - 2 < cn.
+  const int cw = 1 + (c1 ? 1 : 0) + (c2 ? 1 : 0);
+  int cn = 0;
+  uint32_t pcb = 0;
   auto slot_word = [&](int j, int w) -> uint64_t {
-    if (j >= 2) return sl_ld(j, w);
+    if (j >= 2) {
+      if (j - 2 < cn) return L.pcache[pcb + (uint32_t)((j - 2) * cw + (w == 0 ? 0 : w - 1))];
+      return sl_ld(j, w);
+    }
     const uint64_t m0 = 0ull - (uint64_t)(j == 0), m1 = ~m0;
     const uint64_t w0 = 0ull - (uint64_t)(w == 0), w2 = 0ull - (uint64_t)(w == 2);
     const uint64_t w3 = 0ull - (uint64_t)(w == 3);
@@ -576,32 +616,41 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       }
     }
     if (klane) {
+      if (tid == 0) L.pc_used = 0;
       L.kfb[tid] = kNoB;
       L.klb[tid] = kNoB;
       L.khasa[tid] = 0;
     }
     lds_barrier();
-    // ---- headers of every record of the window in flight at once; key counts
+    // ---- every record of the window in flight at once (one pass over the
+    // scattered segments: the records stay in registers through the sort);
+    // key counts
     uint32_t hk[PER], hs[PER];
-    {
-      uint64_t h[PER];
+    uint4 x[PER];
+    uint64_t y[PER];
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t q = tid + i * NT;
-        h[i] = q < nw ? a.recs[(int64_t)L.wrec[q] * RW] : 0ull;
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t q = tid + i * NT;
+      x[i] = make_uint4(0, 0, 0, 0);
+      y[i] = 0;
+      if (q < nw) {
+        const uint64_t* r = a.recs + (int64_t)L.wrec[q] * RW;
+        x[i] = gload4(r);
+        if (NW > 1) y[i] = r[2];
       }
+    }
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t q = tid + i * NT;
-        hk[i] = rec_key(h[i]);
-        hs[i] = (L.wrec[q < nw ? q : 0] & ~(uint32_t)(kCfTile - 1)) + rec_row(h[i]);
-        if (q < nw) atomicAdd(&L.kstart[hk[i] + 1], 1u);
-      }
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t q = tid + i * NT;
+      const uint64_t h = ((uint64_t)x[i].y << 32) | x[i].x;
+      hk[i] = rec_key(h);
+      hs[i] = (L.wrec[q < nw ? q : 0] & ~(uint32_t)(kCfTile - 1)) + rec_row(h);
+      if (q < nw) atomicAdd(&L.kstart[hk[i] + 1], 1u);
     }
     lds_barrier();
     CF_STAMP(wi * 8 + 2);
     // ---- counting sort by key of (seq, key, slot) entries, then each entry's
-    // arrival rank inside its key run -> sorted position
+    // arrival rank inside its key run -> sorted position of window slot q
     {
       const uint32_t c = tid < kpb ? L.kstart[tid + 1] : 0u;
       uint32_t total;
@@ -630,36 +679,21 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
       uint32_t rank = 0;
       for (uint32_t j = r0; j < r1; ++j) rank += (L.kent[j] >> 20) < (e >> 20) ? 1u : 0u;
-      L.sorted[r0 + rank] = (uint16_t)(e & 0x7ffu);
+      L.sorted[e & 0x7ffu] = (uint16_t)(r0 + rank);
     }
     lds_barrier();
-    // ---- full records re-read (L2) in sorted order -> contiguous LDS arrays
+    // ---- the records (registers) -> contiguous LDS arrays in sorted order
     {
-      uint4 x[PER];
-      uint64_t y[PER];
-      uint32_t gr[PER];
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        const uint32_t s = tid + i * NT;
-        x[i] = make_uint4(0, 0, 0, 0);
-        y[i] = 0;
-        gr[i] = 0;
-        if (s < nw) {
-          gr[i] = L.wrec[L.sorted[s]];
-          const uint64_t* r = a.recs + (int64_t)gr[i] * RW;
-          x[i] = gload4(r);
-          if (NW > 1) y[i] = r[2];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t s = tid + i * NT;
-        if (s >= nw) continue;
+        const uint32_t q = tid + i * NT;
+        if (q >= nw) continue;
+        const uint32_t s = L.sorted[q];
         const uint64_t w0 = ((uint64_t)x[i].y << 32) | x[i].x;
         L.sts[s] = x[i].x;
-        L.sseq[s] = (gr[i] & ~(uint32_t)(kCfTile - 1)) + rec_row(w0);
+        L.sseq[s] = hs[i];
         if (a.in_seq)   // received records: global arrival number - chunk base
-          L.sseq[s] = (uint32_t)((int64_t)a.in_seq[(int64_t)L.sseq[s] * a.in_rec_words] - seq_base);
+          L.sseq[s] = (uint32_t)((int64_t)a.in_seq[(int64_t)hs[i] * a.in_rec_words] - seq_base);
         L.skr[s] = (uint16_t)(rec_key(w0) | (rec_role(w0) << 12));
         if (NW > 0) L.scap[0][s] = ((uint64_t)x[i].w << 32) | x[i].z;
         if (NW > 1) L.scap[NW > 1 ? 1 : 0][s] = y[i];
@@ -701,6 +735,36 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     if (klane) {
       r0 = L.kstart[tid];
       r1 = L.kstart[tid + 1];
+      cn = 0;
+      if (r1 > r0 && n > 2) {
+        // slots >= 2 -> pcache (wrec is dead from here to the next window);
+        // a lane that finds pcache full reads HBM instead
+        const uint32_t need = (uint32_t)((n - 2) * cw);
+        const uint32_t off = atomicAdd(&L.pc_used, need);
+        if (off + need <= (uint32_t)(WIN / 2)) {
+          pcb = off;
+          cn = n - 2;
+          for (int j0 = 2; j0 < n; j0 += 4) {
+            uint64_t v0[4], v1[4], v2[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int j = j0 + u;
+              v0[u] = j < n ? sl_ld(j, 0) : 0ull;
+              v1[u] = (j < n && c1) ? sl_ld(j, 2) : 0ull;
+              v2[u] = (j < n && c2) ? sl_ld(j, 3) : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int j = j0 + u;
+              if (j >= n) break;
+              const uint32_t o = off + (uint32_t)((j - 2) * cw);
+              L.pcache[o] = v0[u];
+              if (c1) L.pcache[o + 1] = v1[u];
+              if (c2) L.pcache[o + 1 + (c1 ? 1 : 0)] = v2[u];
+            }
+          }
+        }
+      }
       const uint16_t fb = L.kfb[tid];
       if (r1 > r0 && fb != kNoB && n > 0) {
         const int64_t tb = ts_base + (int64_t)L.sts[fb];
@@ -758,6 +822,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         off += vals[i];
       }
       if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
+      if (tid == 0) { CF_COUNT(1, total); CF_COUNT(5, 1); }
     }
     lds_barrier();
     CF_STAMP(wi * 8 + 5);
@@ -772,7 +837,10 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       const int64_t kl = ((int64_t)tid << lg) | bucket;
       const int64_t kv = kl * p.key_stride + p.key_offset;
       const uint16_t fb = L.kfb[tid], lb = L.klb[tid];
+      CF_COUNT(7, 1);
+      if (n > 2) CF_COUNT(2, 1);
       if (cm) {
+        CF_COUNT(0, cm);
         const int64_t bts = ts_base + (int64_t)L.sts[fb];
         const uint64_t b0 = NW > 0 ? L.scap[0][fb] : 0ull, b1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][fb] : 0ull;
         for (int j = 0; j < cm; ++j) {
@@ -797,17 +865,24 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         t1r = (ts & m1) | (t1r & ~m1);
         a1c0 = (x0 & m1) | (a1c0 & ~m1);
         a1c1 = (x1 & m1) | (a1c1 & ~m1);
-        sl_st(nn, 0, ts);
-        if (c1) sl_st(nn, 2, x0);
-        if (c2) sl_st(nn, 3, x1);
+        if (nn >= 2) CF_COUNT(4, 1);
+        if (nn >= 2) {   // slots 0 / 1 are stored once, at kernel end
+          sl_st(nn, 0, ts);
+          if (c1) sl_st(nn, 2, x0);
+          if (c2) sl_st(nn, 3, x1);
+        }
         ++nn;
+        dirty = true;
       };
-      if (lb == kNoB) {
+      if (lb == kNoB && (a.ablate & 1)) {
+        nn = 0;
+      } else if (lb == kNoB) {
         int drop = 0;
         while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
         if (drop == 0) {
           nn = n;   // unchanged, in place
         } else {
+          if (n > 2) CF_COUNT(3, 1);
           for (int j = drop; j < n; ++j) {
             const uint64_t ts = slot_word(j, 0);
             const uint64_t x0 = c1 ? slot_word(j, 2) : 0ull, x1 = c2 ? slot_word(j, 3) : 0ull;
@@ -817,7 +892,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       }
       // partials created after the last B (a record that is both B and A
       // starts a partial after completing others)
-      for (uint32_t q = (lb == kNoB ? r0 : (uint32_t)lb); q < r1; ++q) {
+      for (uint32_t q = (lb == kNoB ? r0 : (uint32_t)lb); q < r1 && !(a.ablate & 2); ++q) {
         if (!((L.skr[q] >> 12) & ROLE_A)) continue;
         const int64_t ats = ts_base + (int64_t)L.sts[q];
         if (prune && last_a_ts - ats > W) continue;
@@ -829,9 +904,9 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         put_slot((uint64_t)ats, cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1),
                  cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
       }
+      dirty |= nn != n;
       n = nn;
       hdr = (hdr & ~0xffu) | (uint32_t)nn;
-      a.khdr[kidx] = hdr;
     }
     CF_STAMP(wi * 8 + 6);
 
@@ -874,6 +949,20 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     lds_barrier();
     for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
     lds_barrier();
+  }
+  // ---- the key's header and register-resident slots 0 / 1, once
+  if (klane && dirty) {
+    if (n > 0) {
+      sl_st(0, 0, t0r);
+      if (c1) sl_st(0, 2, a0c0);
+      if (c2) sl_st(0, 3, a0c1);
+    }
+    if (n > 1) {
+      sl_st(1, 0, t1r);
+      if (c1) sl_st(1, 2, a1c0);
+      if (c2) sl_st(1, 3, a1c1);
+    }
+    a.khdr[kidx] = hdr;
   }
 }
 

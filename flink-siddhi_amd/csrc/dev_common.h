@@ -110,6 +110,24 @@ __device__ __forceinline__ uint64_t pick(const uint64_t (&v)[kPref][N], int slot
   return x;
 }
 
+// Rows of prefetched slot `slot` (uniform): one uniform branch per slot value,
+// so only the taken slot's copies execute.  A select chain or masked OR over
+// every slot costs kPref times the VALU per row; the empty asm keeps each
+// branch a branch (it is not if-converted into selects).
+template <int N>
+__device__ __forceinline__ void take_slot(const uint64_t (&v)[kPref][N], int slot, uint64_t (&out)[N]) {
+#pragma unroll
+  for (int e = 0; e < N; ++e) out[e] = 0;
+#pragma unroll
+  for (int q = 0; q < kPref; ++q) {
+    if (slot == q) {
+      asm volatile("");
+#pragma unroll
+      for (int e = 0; e < N; ++e) out[e] = v[q][e];
+    }
+  }
+}
+
 // Term-list predicate over prefetched rows (eval_terms_run without loads).
 template <int N>
 __device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const int32_t* slot,

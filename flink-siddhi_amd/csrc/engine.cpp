@@ -370,7 +370,7 @@ int create_runtime(cep_app* a) {
         cols.push_back(c);
         return (int)cols.size() - 1;
       };
-      pf.key_slot = q.key_col_a >= 0 ? slot(q.key_col_a) : -1;
+      pf.key_slot = q.key_col_a >= 0 ? slot(q.key_col_a) : -1;   // slot 0: k_cfpart reads it there
       if (q.f.off >= 0)
         for (int i = 0; i < q.f_terms.n; ++i) pf.f_slot[i] = slot(q.f_terms.t[i].col);
       if (q.g_raw.off >= 0)
@@ -795,7 +795,7 @@ void cep_destroy(cep_app* a) {
   if (a->stamps.p && !a->pats.empty()) {
     // diagnostics: mean duration of each k_walk phase over the last launch's blocks
     const int nb = 1 << a->pats[0].pa.buckets_log2;
-    std::vector<uint64_t> st((size_t)nb * 16);
+    std::vector<uint64_t> st((size_t)4096 * 16);
     hipMemcpy(st.data(), a->stamps.p, st.size() * 8, hipMemcpyDeviceToHost);
     // phases 1..7 of window 0, then phases 2..7 of window 1 (stamps 10..15,
     // relative to window 0's last stamp); blocks with one window have zeros
@@ -817,6 +817,13 @@ void cep_destroy(cep_app* a) {
     std::fprintf(stderr, "\n[cep stamps] walk window1 (%d blocks):", n1);
     for (int i = 10; i < 16; ++i) std::fprintf(stderr, " p%d=%.0f", i - 8, n1 ? sum[i] / n1 : 0.0);
     std::fprintf(stderr, "\n");
+    const uint64_t* c = &st[(size_t)4095 * 16];
+    if (nb <= 4095 && (c[5] || c[7]))
+      std::fprintf(stderr, "[cep counters] walk: carried=%llu all=%llu keylanes_n>2=%llu drop_n>2=%llu "
+                   "slot_st>=2=%llu windows=%llu keylanes=%llu\n",
+                   (unsigned long long)c[0], (unsigned long long)c[1], (unsigned long long)c[2],
+                   (unsigned long long)c[3], (unsigned long long)c[4], (unsigned long long)c[5],
+                   (unsigned long long)c[7]);
     const bool cf = a->pats[0].cf;
     const int nt = (int)std::min<int64_t>(4096, cf ? a->pats[0].cf_chunk / kCfTile
                                                    : a->pats[0].chunk / (kPartThreads * kPartItems));
