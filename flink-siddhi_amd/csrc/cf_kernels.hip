@@ -701,6 +701,30 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     }
     lds_barrier();
     CF_STAMP(wi * 8 + 3);
+    // ---- key lanes: slots >= 2 of the pending list -> pcache (wrec is dead
+    // from here to the next window).  The first two are loaded now and
+    // written after the position scan below, so their latency is hidden; a
+    // lane that finds pcache full reads HBM instead.
+    cn = 0;
+    uint64_t pv0[2], pv1[2], pv2[2];
+    uint32_t pco = 0;
+    const bool fill = klane && n > 2 && L.kstart[tid + 1] > L.kstart[tid];
+    if (fill) {
+      const uint32_t need = (uint32_t)((n - 2) * cw);
+      pco = atomicAdd(&L.pc_used, need);
+      if (pco + need <= (uint32_t)(WIN / 2)) {
+        pcb = pco;
+        cn = n - 2;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = 2 + u;
+      const bool ld = cn > 0 && j < n;
+      pv0[u] = ld ? sl_ld(j, 0) : 0ull;
+      pv1[u] = (ld && c1) ? sl_ld(j, 2) : 0ull;
+      pv2[u] = (ld && c2) ? sl_ld(j, 3) : 0ull;
+    }
     // ---- per sorted position: next B of the run, first / last B, last A
 #pragma unroll 1
     for (int i = 0; i < PER; ++i) {
@@ -727,6 +751,19 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       if ((role & ROLE_B) && nb == kNoB) L.klb[k] = (uint16_t)s;
       if (s == L.kstart[k]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)s : nb;
     }
+    if (cn > 0) {
+      auto put_pc = [&](int j, uint64_t t, uint64_t x0, uint64_t x1) {
+        const uint32_t o = pcb + (uint32_t)((j - 2) * cw);
+        L.pcache[o] = t;
+        if (c1) L.pcache[o + 1] = x0;
+        if (c2) L.pcache[o + 1 + (c1 ? 1 : 0)] = x1;
+      };
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (2 + u < n) put_pc(2 + u, pv0[u], pv1[u], pv2[u]);
+      for (int j = 4; j < n; ++j)   // long lists (rare)
+        put_pc(j, sl_ld(j, 0), c1 ? sl_ld(j, 2) : 0ull, c2 ? sl_ld(j, 3) : 0ull);
+    }
     lds_barrier();
     // ---- key lanes: carried partials completed by the run's first B
     uint32_t r0 = 0, r1 = 0;
@@ -735,36 +772,6 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     if (klane) {
       r0 = L.kstart[tid];
       r1 = L.kstart[tid + 1];
-      cn = 0;
-      if (r1 > r0 && n > 2) {
-        // slots >= 2 -> pcache (wrec is dead from here to the next window);
-        // a lane that finds pcache full reads HBM instead
-        const uint32_t need = (uint32_t)((n - 2) * cw);
-        const uint32_t off = atomicAdd(&L.pc_used, need);
-        if (off + need <= (uint32_t)(WIN / 2)) {
-          pcb = off;
-          cn = n - 2;
-          for (int j0 = 2; j0 < n; j0 += 4) {
-            uint64_t v0[4], v1[4], v2[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int j = j0 + u;
-              v0[u] = j < n ? sl_ld(j, 0) : 0ull;
-              v1[u] = (j < n && c1) ? sl_ld(j, 2) : 0ull;
-              v2[u] = (j < n && c2) ? sl_ld(j, 3) : 0ull;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int j = j0 + u;
-              if (j >= n) break;
-              const uint32_t o = off + (uint32_t)((j - 2) * cw);
-              L.pcache[o] = v0[u];
-              if (c1) L.pcache[o + 1] = v1[u];
-              if (c2) L.pcache[o + 1 + (c1 ? 1 : 0)] = v2[u];
-            }
-          }
-        }
-      }
       const uint16_t fb = L.kfb[tid];
       if (r1 > r0 && fb != kNoB && n > 0) {
         const int64_t tb = ts_base + (int64_t)L.sts[fb];
