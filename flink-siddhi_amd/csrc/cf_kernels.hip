@@ -102,6 +102,53 @@ __device__ __forceinline__ void pick_carried(const uint64_t (&pv)[kPref][E], int
   }
 }
 
+// Columns of a lane's E rows (row0 + 64 e) for the fast paths: event ts,
+// stream handle and every prefetched slot, all loads issued before any use;
+// unused slots and the ts alias issue none (uniform branches).
+template <int E>
+__device__ __forceinline__ void cf_load_cols(const RowsArgs& rows, const PrefPlan& pref, int ts_slot,
+                                             int64_t row0, uint32_t valid, uint64_t (&tsv)[E],
+                                             uint32_t (&sb)[E], uint64_t (&pv)[kPref][E]) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const bool ok = (valid >> e) & 1u;
+    tsv[e] = ok ? (uint64_t)rows.ts[row0 + 64 * e] : 0ull;
+    sb[e] = (ok && rows.stream) ? (uint32_t)rows.stream[row0 + 64 * e] : (uint32_t)rows.input;
+  }
+#pragma unroll
+  for (int q = 0; q < kPref; ++q) {
+    const int c = pref.col[q];
+    const int ty = rows.cols.t[c];
+    if (q < pref.n && q != ts_slot) {
+      const void* base = rows.cols.p[c];
+      if (ty == T_LONG || ty == T_DOUBLE) {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          pv[q][e] = ((valid >> e) & 1u) ? ((const uint64_t*)base)[row0 + 64 * e] : 0ull;
+      } else if (ty == T_BOOL) {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          pv[q][e] = ((valid >> e) & 1u) ? (((const uint8_t*)base)[row0 + 64 * e] ? 1ull : 0ull) : 0ull;
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t v = ((valid >> e) & 1u) ? ((const uint32_t*)base)[row0 + 64 * e] : 0u;
+          pv[q][e] = ty == T_FLOAT ? (uint64_t)v : from_i32((int32_t)v);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) pv[q][e] = 0;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPref; ++q)
+    if (q == ts_slot) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) pv[q][e] = tsv[e];
+    }
+}
+
 // Record field accessors (w0).
 __device__ __forceinline__ uint32_t rec_row(uint64_t w0) { return (uint32_t)(w0 >> 32) & 0x1fffu; }
 __device__ __forceinline__ uint32_t rec_role(uint64_t w0) { return (uint32_t)(w0 >> 45) & 0x7u; }
@@ -182,47 +229,8 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     }
   }
   if (!FR && valid) {
-    // every load of the lane's rows is issued before any use; unused slots
-    // and the ts alias issue none (uniform branches)
     uint32_t sb[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const bool ok = (valid >> e) & 1u;
-      tsv[e] = ok ? (uint64_t)a.rows.ts[row0 + 64 * e] : 0ull;
-      sb[e] = (ok && a.rows.stream) ? (uint32_t)a.rows.stream[row0 + 64 * e] : (uint32_t)a.rows.input;
-    }
-#pragma unroll
-    for (int q = 0; q < kPref; ++q) {
-      const int c = a.pref.col[q];
-      const int ty = a.rows.cols.t[c];
-      if (q < a.pref.n && q != a.ts_slot) {
-        const void* base = a.rows.cols.p[c];
-        if (ty == T_LONG || ty == T_DOUBLE) {
-#pragma unroll
-          for (int e = 0; e < E; ++e)
-            pv[q][e] = ((valid >> e) & 1u) ? ((const uint64_t*)base)[row0 + 64 * e] : 0ull;
-        } else if (ty == T_BOOL) {
-#pragma unroll
-          for (int e = 0; e < E; ++e)
-            pv[q][e] = ((valid >> e) & 1u) ? (((const uint8_t*)base)[row0 + 64 * e] ? 1ull : 0ull) : 0ull;
-        } else {
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const uint32_t v = ((valid >> e) & 1u) ? ((const uint32_t*)base)[row0 + 64 * e] : 0u;
-            pv[q][e] = ty == T_FLOAT ? (uint64_t)v : from_i32((int32_t)v);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) pv[q][e] = 0;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < kPref; ++q)
-      if (q == a.ts_slot) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) pv[q][e] = tsv[e];
-      }
+    cf_load_cols<E>(a.rows, a.pref, a.ts_slot, row0, valid, tsv, sb, pv);
     uint32_t is_a = 0, is_b = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -347,6 +355,185 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     }
   }
   CF_STAMP(5);
+}
+
+// ============================================================= k_cfroute ==
+// Sender side of the key shuffle: the k_cfpart load path,
+// predicate push-down (rows no state can use are not shipped), owner =
+// key % world, owner ranks stable in arrival order (wave ballots per owner,
+// then a prefix over waves), wide records [key | role << 32 | stream << 40,
+// global seq, ts, logical carried words] staged in LDS and stored as one
+// contiguous owner-grouped run per tile.  k_route_scan / k_route_gather
+// (kernels.hip) then make each owner's records contiguous.
+constexpr int kCfRouteStage = 112 * 1024;   // bytes of staged wide records
+constexpr int kRouteSmallWorld = 8;          // owners ranked with scalar counters
+__global__ __launch_bounds__(kCfPartThreads, 1) void k_cfroute(CfRouteArgs ca) {
+  constexpr int E = kCfItems, NT = kCfPartThreads, NWV = NT / 64;
+  const RouteArgs& a = ca.r;
+  const PatternArgs& p = a.pat;
+  __shared__ uint32_t wcnt[NWV][kMaxWorld];   // per wave, per owner: rows so far / then wave base
+  __shared__ uint32_t obase[kMaxWorld + 1];   // owner segment starts in the tile
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kCfRouteStage / 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int world = a.world, wrw = a.wrw;
+  const int64_t tile = blockIdx.x;
+  for (int i = tid; i < NWV * kMaxWorld; i += NT) wcnt[i / kMaxWorld][i % kMaxWorld] = 0;
+
+  const int64_t r0 = tile * kCfTile + (int64_t)wave * 64 * E + lane;
+  const int64_t row0 = a.rows.row0 + r0;
+  uint32_t valid = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) valid |= (r0 + 64 * e < a.rows.n ? 1u : 0u) << e;
+  uint64_t tsv[E], pv[kPref][E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) tsv[e] = 0;
+  uint32_t is_a = 0, role_a = 0, role_b = 0, role_g = 0;
+  uint64_t fkey[E], fc0[E], fc1[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) fkey[e] = fc0[e] = fc1[e] = 0;
+  if (valid) {
+    uint32_t sb[E];
+    cf_load_cols<E>(a.rows, ca.pref, ca.ts_slot, row0, valid, tsv, sb, pv);
+    uint32_t is_b = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if ((valid >> e) & 1u) {
+        is_a |= ((int)sb[e] == p.a_stream ? 1u : 0u) << e;
+        is_b |= ((int)sb[e] == p.b_stream ? 1u : 0u) << e;
+      }
+    }
+    const uint32_t all = (1u << E) - 1u;
+    if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E>(p.f_terms, ca.pref.f_slot, a.rows.cols, pv));
+    if (is_b) {
+      if (p.g_walk_prog >= 0) {   // g reads s1: decided by the owner's walk
+        role_b = is_b;
+      } else {
+        role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, ca.pref.g_slot, a.rows.cols, pv));
+        role_g = role_b;
+      }
+    }
+    // logical carried words: the A stream's columns on A rows, else the B's
+    if (p.nrec_a > 0 || p.nrec_b > 0)
+      pick_carried<E>(pv, p.nrec_a > 0 ? ca.pref.reca_slot[0] : -1, p.nrec_b > 0 ? ca.pref.recb_slot[0] : -1,
+                      is_a, fc0);
+    if (p.nrec_a > 1 || p.nrec_b > 1)
+      pick_carried<E>(pv, p.nrec_a > 1 ? ca.pref.reca_slot[1] : -1, p.nrec_b > 1 ? ca.pref.recb_slot[1] : -1,
+                      is_a, fc1);
+    if (ca.pref.key_slot >= 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) fkey[e] = pv[0][e];
+    }
+  }
+  __syncthreads();   // wcnt zeroed
+
+  // owner per kept row, stable rank inside (wave, owner): rows of a wave are
+  // in arrival order by (e, lane)
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int dest[E];
+  uint32_t wr[E];
+  uint32_t pre[kRouteSmallWorld];   // world <= 8: rows per owner so far in this wave (uniform)
+#pragma unroll
+  for (int d = 0; d < kRouteSmallWorld; ++d) pre[d] = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    dest[e] = -1;
+    wr[e] = 0;
+    if ((((role_a | role_b) >> e) & 1u)) {
+      const int64_t key = (int64_t)fkey[e];
+      if (key < 0 || key > 0xffffffffll) set_err(a.err, ERR_KEY_RANGE);
+      else dest[e] = (int)((uint32_t)key % (uint32_t)world);
+    }
+    if (world > kRouteSmallWorld) {
+      // owners met in this row group, one at a time (counts in LDS)
+      uint64_t rem = __ballot(dest[e] >= 0);
+      while (rem) {
+        const int leader = __ffsll((long long)rem) - 1;
+        const int d0 = __shfl(dest[e], leader, 64);
+        const uint64_t m = __ballot(dest[e] == d0);
+        const uint32_t c0 = wcnt[wave][d0];
+        if (dest[e] == d0) wr[e] = c0 + (uint32_t)__popcll(m & lt);
+        if (lane == leader) wcnt[wave][d0] = c0 + (uint32_t)__popcll(m);
+        rem &= ~m;
+      }
+    } else {
+      // every owner, counts in scalar registers: no LDS round trip per owner
+#pragma unroll
+      for (int d = 0; d < kRouteSmallWorld; ++d) {
+        const uint64_t m = __ballot(dest[e] == d);
+        if (dest[e] == d) wr[e] = pre[d] + (uint32_t)__popcll(m & lt);
+        pre[d] += (uint32_t)__popcll(m);
+      }
+    }
+  }
+  if (world <= kRouteSmallWorld) {
+    uint32_t mine = 0;
+#pragma unroll
+    for (int d = 0; d < kRouteSmallWorld; ++d) mine = lane == d ? pre[d] : mine;
+    if (lane < kRouteSmallWorld) wcnt[wave][lane] = mine;
+  }
+  __syncthreads();
+  // tile totals per owner -> owner segment starts; per (wave, owner) bases
+  if (tid < 64) {
+    uint32_t tot = 0;
+    if (tid < world)
+      for (int w = 0; w < NWV; ++w) tot += wcnt[w][tid];
+    uint32_t x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (tid < world) {
+      obase[tid] = x - tot;
+      a.tcount[tile * world + tid] = tot;
+    }
+    if (tid == 63) obase[world] = x;   // kept rows of the tile
+  }
+  __syncthreads();
+  if (tid < world) {
+    uint32_t run = obase[tid];
+    for (int w = 0; w < NWV; ++w) {
+      const uint32_t c = wcnt[w][tid];
+      wcnt[w][tid] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = obase[world];
+  const bool staged = (int64_t)total * wrw * 8 <= kCfRouteStage;   // uniform
+  uint64_t* tout = a.arena + tile * (int64_t)kCfTile * wrw;
+  const int nrc = wrw - 3;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (dest[e] < 0) continue;
+    const uint32_t pos = wcnt[wave][dest[e]] + wr[e];
+    const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
+                          ((role_g >> e) & 1u) * ROLE_G;
+    const int64_t r = row0 + 64 * e;
+    uint64_t w[5];
+    const uint32_t sid = ((is_a >> e) & 1u) ? (uint32_t)p.a_stream : (uint32_t)p.b_stream;   // kept rows are A or B
+    w[0] = (uint64_t)(uint32_t)fkey[e] | ((uint64_t)role << 32) | ((uint64_t)sid << 40);
+    w[1] = (uint64_t)(a.seq0 + (r - a.rows.row0));
+    w[2] = tsv[e];
+    w[3] = fc0[e];
+    w[4] = fc1[e];
+    uint64_t* o = staged ? stage + (int64_t)pos * wrw : tout + (int64_t)pos * wrw;
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+      if (c < 3 + nrc) o[c] = w[c];
+  }
+  if (staged) {
+    __syncthreads();
+    const int64_t words = (int64_t)total * wrw;
+    for (int64_t w = 2 * tid; w < words; w += 2 * NT) {
+      if (w + 1 < words) *(uint4*)(tout + w) = *(const uint4*)(stage + w);
+      else tout[w] = stage[w];
+    }
+  }
+}
+
+void launch_cf_route(const CfRouteArgs& a, int64_t ntiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_cfroute, dim3((unsigned)ntiles), dim3(kCfPartThreads), 0, s, a);
 }
 
 // ============================================================== k_cfwalk ==

@@ -1251,7 +1251,12 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   RowsArgs rows{};
   int rc = batch_rows(a, b, &rows);
   if (rc) return rc;
-  const int64_t tile_rows = kPartThreads * kPartItems;
+  // fast route (k_cfroute) when every column the pattern reads is prefetchable
+  // and f / g are term lists (the k_cfpart load path); CEP_NO_CF=1 forces k_route
+  static const bool no_cf = std::getenv("CEP_NO_CF") != nullptr;
+  const bool fast = !no_cf && !rt.part_vm && rt.pref.n >= 0 && rt.pref.key_slot <= 0 &&
+                    rt.pa.rec_words + 1 <= 5 && pref_aligned(rt.pref, rows);
+  const int64_t tile_rows = fast ? kCfTile : kPartThreads * kPartItems;
   const int64_t ntiles = (b->n + tile_rows - 1) / tile_rows;
   const int wrw = rt.pa.rec_words + 1;
   if (!dev_ensure(&a->route_arena, (size_t)ntiles * tile_rows * wrw * 8, a->stream, false) ||
@@ -1272,8 +1277,21 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   ra.err = (unsigned int*)a->err.p;
   {
     LaunchTimer t(a, CEP_K_ROUTE);
-    launch_route(ra, ntiles, rt.part_vm, (uint32_t*)a->route_toffs.p,
-                 (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
+    if (fast) {
+      CfRouteArgs ca{};
+      ca.r = ra;
+      ca.pref = rt.pref;
+      ca.ts_slot = -1;
+      for (int i = 0; i < rt.pref.n; ++i)
+        if (rows.cols.p[rt.pref.col[i]] == (const void*)rows.ts && rows.cols.t[rt.pref.col[i]] == T_LONG)
+          ca.ts_slot = i;
+      launch_cf_route(ca, ntiles, a->stream);
+      launch_route_collect(ra, ntiles, (uint32_t*)a->route_toffs.p,
+                           (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
+    } else {
+      launch_route(ra, ntiles, rt.part_vm, (uint32_t*)a->route_toffs.p,
+                   (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
+    }
   }
   // counts first: the gather must not overrun rec_out
   std::vector<unsigned long long> dc(world);

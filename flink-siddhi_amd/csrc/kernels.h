@@ -245,6 +245,14 @@ struct CfWalkArgs {
   unsigned int* err;
 };
 
+// Fast route (k_cfroute): the k_cfpart load path for the sender side of the
+// key shuffle (8192-row tiles, prefetched columns, term-list f / g).
+struct CfRouteArgs {
+  RouteArgs r;                 // r.tile_rows = kCfTile
+  PrefPlan pref;
+  int32_t ts_slot;             // prefetch slot whose column IS the event-ts buffer (-1: none)
+};
+
 // --------------------------------------------------------------- launchers --
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
@@ -252,6 +260,9 @@ void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
                   unsigned long long* dcount, uint64_t* out, hipStream_t s);
+void launch_route_collect(const RouteArgs& a, int64_t ntiles, uint32_t* toffs,
+                          unsigned long long* dcount, uint64_t* out, hipStream_t s);
+void launch_cf_route(const CfRouteArgs& a, int64_t ntiles, hipStream_t s);
 void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s);
 void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
                      int64_t rate, int64_t t0, int single_stream, int32_t* key,

@@ -743,6 +743,12 @@ void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
                   unsigned long long* dcount, uint64_t* out, hipStream_t s) {
   if (vm) hipLaunchKernelGGL(k_route<true>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
   else hipLaunchKernelGGL(k_route<false>, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+  launch_route_collect(a, ntiles, toffs, dcount, out, s);
+}
+
+// Owner-contiguous output from per-tile owner segments (k_route / k_cfroute).
+void launch_route_collect(const RouteArgs& a, int64_t ntiles, uint32_t* toffs,
+                          unsigned long long* dcount, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_route_scan, dim3((unsigned)a.world), dim3(512), 0, s, a.tcount, ntiles, a.world,
                      toffs, dcount);
   hipLaunchKernelGGL(k_route_gather, dim3((unsigned)ntiles), dim3(256), 0, s, a, ntiles, toffs, dcount, out);

@@ -64,3 +64,28 @@ def test_route_exchange_matches_oracle(world, path, monkeypatch):
     assert_same_rows(got, want, "shuffle world=%d" % world)
     for rt in owners + [sender]:
         rt.shutdown()
+
+
+@pytest.mark.parametrize("world", [4, 11])
+def test_fast_route_equals_general_route(world, monkeypatch):
+    # k_cfroute (8192-row tiles, scalar owner counters for world <= 8, LDS
+    # counters above) and k_route (CEP_NO_CF=1) ship identical records
+    n, keys = 50000, 4096
+    w = workload.generate(0, n, keys, rate=1)
+    d = _dev(w)
+    got = {}
+    for path in ("cf", "general"):
+        if path == "general":
+            monkeypatch.setenv("CEP_NO_CF", "1")
+        else:
+            monkeypatch.delenv("CEP_NO_CF", raising=False)
+        rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+        recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
+                                seq0=7, streams=d["stream"])
+        got[path] = (recs[:sum(counts)].cpu().numpy().copy(), counts)
+        rt.shutdown()
+    (ra, ca), (rb, cb) = got["cf"], got["general"]
+    assert ca == cb and sum(ca) > 1000
+    assert (ra[:, :4] == rb[:, :4]).all()
+    is_b = ((ra[:, 0] >> 40) & 0xff) == 1
+    assert (ra[is_b, 4] == rb[is_b, 4]).all()
