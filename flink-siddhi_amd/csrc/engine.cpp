@@ -107,6 +107,7 @@ struct cep_app {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;    // partition pass of the next chunk
   hipEvent_t in_ready = nullptr;
+  hipEvent_t ext_ready = nullptr;   // cep_stream_wait: producer stream of device inputs
   bool enabled = true;
   std::string last_error;
   std::vector<std::string> dict;
@@ -225,7 +226,8 @@ int create_runtime(cep_app* a) {
                                      prop.gcnArchName);
   if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&a->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&a->in_ready, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&a->in_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&a->ext_ready, hipEventDisableTiming) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
@@ -878,6 +880,7 @@ void cep_destroy(cep_app* a) {
       if (p.walk_done[b]) hipEventDestroy(p.walk_done[b]);
     }
   if (a->in_ready) hipEventDestroy(a->in_ready);
+  if (a->ext_ready) hipEventDestroy(a->ext_ready);
   if (a->side) hipStreamDestroy(a->side);
   if (a->stream) hipStreamDestroy(a->stream);
   delete a;
@@ -1072,6 +1075,14 @@ int cep_reset_output(cep_app* a) {
     hipMemsetAsync(o.count, 0, sizeof(unsigned long long), a->stream);
     o.bound = 0;
   }
+  return CEP_OK;
+}
+
+int cep_stream_wait(cep_app* a, void* hip_stream) {
+  if (!a) return CEP_E_ARG;
+  if (hipEventRecord(a->ext_ready, (hipStream_t)hip_stream) != hipSuccess ||
+      hipStreamWaitEvent(a->stream, a->ext_ready, 0) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "cep_stream_wait: invalid stream");
   return CEP_OK;
 }
 

@@ -142,6 +142,7 @@ SIGNATURES = {
     "cep_restore": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "cep_free": (None, [C.c_void_p]),
     "cep_set_enabled": (C.c_int, [C.c_void_p, C.c_int]),
+    "cep_stream_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
     "cep_dict_intern": (C.c_int32, [C.c_void_p, C.c_char_p]),
     "cep_dict_lookup": (C.c_char_p, [C.c_void_p, C.c_int32]),
     "cep_stats": (C.c_int, [C.c_void_p, C.POINTER(cep_stats_t)]),

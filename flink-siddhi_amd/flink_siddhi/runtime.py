@@ -184,7 +184,16 @@ class SiddhiAppRuntime:
             keep.append(k)
         b = L.cep_batch(n=_len(ts), ts=tsp, stream=sp, input=h, ncols=len(cols),
                         cols=ptrs, on_device=1 if on_device else 0)
+        if on_device:
+            self._wait_producer(ts)
         self._check(self._lib.cep_send_batch(self._h, C.byref(b)))
+
+    def _wait_producer(self, t):
+        """Order the engine's stream after torch's current stream (device
+        inputs may still be in flight there: generators, copies, RCCL)."""
+        import torch
+        s = torch.cuda.current_stream(t.device).cuda_stream
+        self._check(self._lib.cep_stream_wait(self._h, C.c_void_p(s)))
 
     def flush(self):
         self._check(self._lib.cep_flush(self._h))
@@ -224,6 +233,7 @@ class SiddhiAppRuntime:
         b = L.cep_batch(n=n, ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
                         cols=ptrs, on_device=1)
         counts = (C.c_int64 * world)()
+        self._wait_producer(ts)
         self._check(self._lib.cep_route_batch(self._h, C.byref(b), world, seq0,
                                               C.c_void_p(out.data_ptr()), out.shape[0], counts))
         return out, [int(c) for c in counts]
@@ -231,6 +241,8 @@ class SiddhiAppRuntime:
     def send_records(self, recs, n: int, events_represented: int = 0):
         """Owner side: feed received shuffle records (source-rank order)."""
         p = C.c_void_p(recs.data_ptr()) if n else None
+        if n and getattr(recs, "is_cuda", False):
+            self._wait_producer(recs)
         self._check(self._lib.cep_send_records(self._h, p, n, events_represented))
 
     def output_device(self, out_id: str):

@@ -192,6 +192,13 @@ void cep_free(void* p);
  * events sent while disabled are dropped (:128). */
 int cep_set_enabled(cep_app* app, int enabled);
 
+/* Device inputs produced on another HIP stream (a framework's current stream,
+ * an RCCL collective): the engine's work queued after this call waits for
+ * everything queued on hip_stream so far (event + stream wait, no host
+ * sync).  Call before cep_send_batch / cep_route_batch / cep_send_records
+ * with device pointers whose producer is still in flight. */
+int cep_stream_wait(cep_app* app, void* hip_stream);
+
 /* String dictionary (STRING columns carry int32 ids). */
 int32_t cep_dict_intern(cep_app* app, const char* s);
 const char* cep_dict_lookup(cep_app* app, int32_t id);
