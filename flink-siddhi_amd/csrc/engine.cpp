@@ -519,16 +519,20 @@ bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf, bool from_re
   return true;
 }
 
-// Closed-form fast path: k_cfpart(c+1) on the side stream overlaps
-// k_cfwalk(c) on the main stream (double-buffered arenas).
+// Closed-form fast path: k_cfpart(c) then k_cfwalk(c) per chunk (double-
+// buffered arenas; CEP_OVERLAP=1 runs the partitions on the side stream).
 int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
                    const RowsArgs& rows_all, const CfPlan& cf,
                    const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
   const int P = 1 << rt.pa.buckets_log2;
   hipEventRecord(a->in_ready, a->stream);
   hipStreamWaitEvent(a->side, a->in_ready, 0);
-  static const bool no_overlap = std::getenv("CEP_NO_OVERLAP") != nullptr;
-  hipStream_t side = no_overlap ? a->stream : a->side;
+  // Both passes on the main stream by default: k_cfpart and k_cfwalk cannot
+  // share a CU (each fills its register file), so the side stream only
+  // time-slices them (measured: no throughput gain, inflated kernel times).
+  // CEP_OVERLAP=1 puts the partition on the side stream.
+  static const bool overlap = std::getenv("CEP_OVERLAP") != nullptr;
+  hipStream_t side = overlap ? a->side : a->stream;
   for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.cf_chunk) {
     const int b = rt.cur;
     rt.cur ^= 1;

@@ -8,7 +8,7 @@ for lib in $LIBS; do
 done
 for lib in $LIBS; do
   echo "== $lib" >> gpurun_out/cmp.log
-  CEP_LIB=$GRAFT_REPO_ROOT/flink-siddhi_amd/$lib CEP_NO_OVERLAP=1 timeout -k 10 120 python bench.py --events 134217728 --steps 3 --warmup 1 --no-cpu 2>/dev/null | grep '^{' | python3 -c "
+  CEP_LIB=$GRAFT_REPO_ROOT/flink-siddhi_amd/$lib timeout -k 10 120 python bench.py --events 134217728 --steps 3 --warmup 1 --no-cpu 2>/dev/null | grep '^{' | python3 -c "
 import json,sys;d=json.loads(sys.stdin.read());print('serial', round(d['value']/1e9,2), {k:round(v['avg_us'],1) for k,v in d['kernels'].items()})" >> gpurun_out/cmp.log || exit $?
   CEP_LIB=$GRAFT_REPO_ROOT/flink-siddhi_amd/$lib timeout -k 10 120 python bench.py --no-cpu 2>/dev/null | grep '^{' | python3 -c "
 import json,sys;d=json.loads(sys.stdin.read());print('overlap', round(d['value']/1e9,2), {k:round(v['avg_us'],1) for k,v in d['kernels'].items()})" >> gpurun_out/cmp.log || exit $?
