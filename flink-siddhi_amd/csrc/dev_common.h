@@ -137,8 +137,7 @@ __device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const in
   for (int i = 0; i < tl.n; ++i) {
     const Term& t = tl.t[i];
     uint64_t v[N];
-#pragma unroll
-    for (int e = 0; e < N; ++e) v[e] = pick<N>(vals, slot[i], e);
+    take_slot<N>(vals, slot[i], v);   // one uniform branch, not a masked OR over every slot
     int ty = (t.coltype == T_BOOL || t.coltype == T_STRING) ? T_INT : t.coltype;
     uint32_t nullm = 0;
     if (t.aop) {

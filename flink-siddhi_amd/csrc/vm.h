@@ -338,6 +338,29 @@ __device__ __forceinline__ void convert_run(uint64_t (&v)[N], int from, int to) 
 #define CEP_RUN(expr)                     \
   _Pragma("unroll") for (int e = 0; e < N; ++e) { expr; }
 
+// Unsigned 32-bit division by an invariant divisor d >= 1 (Granlund-
+// Montgomery / "round-up" magic): l = ceil(log2 d), m = floor(2^32 (2^l - d)
+// / d) + 1, n / d = (t + ((n - t) >> 1)) >> (l - 1) with t = mulhi(m, n);
+// exact for every 32-bit n (checked exhaustively over edge and random
+// dividends / divisors).  d = 1 is the identity.
+struct Div32 {
+  uint32_t m;
+  int l;
+};
+__device__ __forceinline__ Div32 div32_magic(uint32_t d) {
+  Div32 r{0u, 0};
+  if (d > 1) {
+    r.l = 32 - __builtin_clz(d - 1u);
+    r.m = (uint32_t)(((((uint64_t)1 << r.l) - d) << 32) / d) + 1u;
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t div32_apply(uint32_t n, uint32_t d, const Div32& dm) {
+  if (d == 1u) return n;
+  const uint32_t t = __umulhi(dm.m, n);
+  return (t + ((n - t) >> 1)) >> (dm.l - 1);
+}
+
 template <int N>
 __device__ __forceinline__ void arith_run(uint64_t (&v)[N], int op, int t, uint64_t k,
                                           uint32_t* nullm) {
@@ -349,15 +372,30 @@ __device__ __forceinline__ void arith_run(uint64_t (&v)[N], int op, int t, uint6
         case OP_SUB: CEP_RUN(v[e] = from_i32((int32_t)((uint32_t)v[e] - (uint32_t)y))) break;
         case OP_MUL: CEP_RUN(v[e] = from_i32((int32_t)((uint32_t)v[e] * (uint32_t)y))) break;
         case OP_DIV:
+        default: {   // OP_MOD
           if (y == 0) { *nullm = ~0u; return; }
-          if (y == -1) { CEP_RUN(v[e] = from_i32((int32_t)(0u - (uint32_t)v[e]))) }
-          else { CEP_RUN(v[e] = from_i32((int32_t)v[e] / y)) }
+          if (y == -1) {
+            if (op == OP_DIV) { CEP_RUN(v[e] = from_i32((int32_t)(0u - (uint32_t)v[e]))) }
+            else { CEP_RUN(v[e] = 0) }
+            return;
+          }
+          // truncated division by a constant (Java int / and %): |x| / |y| by
+          // magic-number multiplication (one mul_hi, exact for every 32-bit
+          // dividend), then the signs — not a division routine per row
+          const uint32_t d = y < 0 ? 0u - (uint32_t)y : (uint32_t)y;
+          const Div32 dm = div32_magic(d);
+          CEP_RUN({
+            const int32_t x = (int32_t)v[e];
+            const uint32_t n = x < 0 ? 0u - (uint32_t)x : (uint32_t)x;
+            const uint32_t q = div32_apply(n, d, dm);
+            if (op == OP_DIV) v[e] = from_i32((int32_t)(((x < 0) != (y < 0)) ? 0u - q : q));
+            else {
+              const uint32_t r = n - q * d;
+              v[e] = from_i32((int32_t)(x < 0 ? 0u - r : r));
+            }
+          })
           break;
-        default:
-          if (y == 0) { *nullm = ~0u; return; }
-          if (y == -1) { CEP_RUN(v[e] = 0) }
-          else { CEP_RUN(v[e] = from_i32((int32_t)v[e] % y)) }
-          break;
+        }
       }
       return;
     }
