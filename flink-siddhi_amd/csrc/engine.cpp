@@ -119,6 +119,17 @@ struct cep_app {
   DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   std::vector<DevBuf> stage;   // host-batch staging columns (+ts, +stream)
+  // event-time reorder buffer (cep_buffer_batch / cep_watermark): rows of
+  // one input layout since the last watermark, SoA in arrival order
+  struct Reorder {
+    int input = -1;            // layout owner (-1: empty)
+    bool has_stream = false;
+    int64_t n = 0, cap = 0;
+    int64_t released_max = INT64_MIN;   // latest ts handed to the engine
+    DevBuf col[kMaxCols], ts, stream;  // buffered rows
+    DevBuf out[kMaxCols], ots, ostream;   // sorted released rows (a device batch)
+    DevBuf keys, idx_in, idx_out, temp, bound;
+  } ro;
   int64_t events_in = 0, matches_out = 0, batches = 0;
   int64_t last_ts = INT64_MIN;
   int64_t launches[16] = {0};
@@ -867,6 +878,13 @@ void cep_destroy(cep_app* a) {
     }
   }
   for (auto& s : a->stage) dev_free(&s);
+  for (int c = 0; c < kMaxCols; ++c) {
+    dev_free(&a->ro.col[c]);
+    dev_free(&a->ro.out[c]);
+  }
+  for (DevBuf* b : {&a->ro.ts, &a->ro.stream, &a->ro.ots, &a->ro.ostream, &a->ro.keys, &a->ro.idx_in,
+                    &a->ro.idx_out, &a->ro.temp, &a->ro.bound})
+    dev_free(b);
   dev_free(&a->code);
   dev_free(&a->konst);
   dev_free(&a->tile_state);
@@ -984,6 +1002,119 @@ int cep_send_batch(cep_app* a, const cep_batch* b) {
   a->batches++;
   rc = send_device_rows(a, rows);
   if (b->on_device == 0) hipStreamSynchronize(a->stream);   // host buffers may be reused
+  return rc;
+}
+
+// ---- event-time reorder (AbstractSiddhiOperator.java:222-231 processElement
+// offers to the PriorityQueue; :238-247 processWatermark drains ts <= mark)
+int cep_buffer_batch(cep_app* a, const cep_batch* b) {
+  if (!a || !b || b->n < 0) return CEP_E_ARG;
+  if (b->n == 0) return CEP_OK;
+  if (b->input < 0 || b->input >= (int)a->app.inputs.size())
+    return fail(a, CEP_E_UNDEFINED_STREAM, "undefined input handle");
+  const StreamSchema& sd = a->app.inputs[b->input];
+  if (b->ncols != (int)sd.attrs.size() || b->ncols > kMaxCols)
+    return fail(a, CEP_E_ARG, "batch has " + std::to_string(b->ncols) + " columns, stream " + sd.id +
+                                  " defines " + std::to_string(sd.attrs.size()));
+  auto& r = a->ro;
+  if (r.n > 0 && (r.input != b->input || r.has_stream != (b->stream != nullptr)))
+    return fail(a, CEP_E_ARG, "the reorder buffer holds rows of another input layout: call cep_watermark first");
+  if (r.n + b->n > (int64_t)INT32_MAX) return fail(a, CEP_E_CAPACITY, "reorder buffer holds at most 2^31-1 rows");
+  r.input = b->input;
+  r.has_stream = b->stream != nullptr;
+  const int64_t need = r.n + b->n;
+  const hipMemcpyKind kind = b->on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  bool ok = true;
+  for (int c = 0; c < b->ncols && ok; ++c) {
+    const int w = type_width(sd.attrs[c].type);
+    ok = dev_ensure(&r.col[c], (size_t)need * w, a->stream, true);
+    if (ok) hipMemcpyAsync((char*)r.col[c].p + r.n * w, b->cols[c], (size_t)b->n * w, kind, a->stream);
+  }
+  ok = ok && dev_ensure(&r.ts, (size_t)need * 8, a->stream, true);
+  if (ok) hipMemcpyAsync((char*)r.ts.p + r.n * 8, b->ts, (size_t)b->n * 8, kind, a->stream);
+  if (ok && b->stream) {
+    ok = dev_ensure(&r.stream, (size_t)need, a->stream, true);
+    if (ok) hipMemcpyAsync((char*)r.stream.p + r.n, b->stream, (size_t)b->n, kind, a->stream);
+  }
+  if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (reorder buffer)");
+  r.n = need;
+  if (!b->on_device) hipStreamSynchronize(a->stream);   // host buffers may be reused
+  return CEP_OK;
+}
+
+int64_t cep_buffered(cep_app* a) { return a ? a->ro.n : -1; }
+
+int cep_watermark(cep_app* a, int64_t mark) {
+  if (!a) return CEP_E_ARG;
+  auto& r = a->ro;
+  if (r.n == 0) return CEP_OK;
+  const StreamSchema& sd = a->app.inputs[r.input];
+  const int nc = (int)sd.attrs.size();
+  const int64_t n = r.n;
+  const size_t tb = reorder_temp_bytes(n);
+  if (!dev_ensure(&r.keys, (size_t)n * 8, a->stream, false) ||
+      !dev_ensure(&r.idx_in, (size_t)n * 4, a->stream, false) ||
+      !dev_ensure(&r.idx_out, (size_t)n * 4, a->stream, false) || !dev_ensure(&r.temp, tb + 16, a->stream, false) ||
+      !dev_ensure(&r.bound, 64, a->stream, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory (reorder sort)");
+  if (reorder_sort(r.temp.p, r.temp.bytes, (const int64_t*)r.ts.p, (int64_t*)r.keys.p, (int32_t*)r.idx_in.p,
+                   (int32_t*)r.idx_out.p, n, a->stream))
+    return fail(a, CEP_E_DEVICE, "reorder sort failed");
+  launch_upper_bound((const int64_t*)r.keys.p, n, mark, (int64_t*)r.bound.p, a->stream);
+  int64_t hb[3] = {0, 0, 0};
+  if (hipMemcpyAsync(hb, r.bound.p, sizeof(hb), hipMemcpyDeviceToHost, a->stream) != hipSuccess ||
+      hipStreamSynchronize(a->stream) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "device failure during processing");
+  const int64_t rel = hb[0];
+  if (rel == 0) return CEP_OK;
+  // a row at or before an earlier watermark arrived late: the reference hands
+  // it to Siddhi out of order; `within` needs event-time order, so refuse
+  if (hb[1] < r.released_max)
+    return fail(a, CEP_E_ARG, "late event: ts " + std::to_string(hb[1]) + " is before already released ts " +
+                                  std::to_string(r.released_max));
+  const int32_t* perm = (const int32_t*)r.idx_out.p;
+  bool ok = true;
+  for (int c = 0; c < nc && ok; ++c) {
+    const int w = type_width(sd.attrs[c].type);
+    ok = dev_ensure(&r.out[c], (size_t)n * w, a->stream, false);
+    if (ok) launch_gather(r.col[c].p, r.out[c].p, perm, 0, n, w, a->stream);
+  }
+  ok = ok && dev_ensure(&r.ots, (size_t)n * 8, a->stream, false);
+  if (ok) hipMemcpyAsync(r.ots.p, r.keys.p, (size_t)n * 8, hipMemcpyDeviceToDevice, a->stream);
+  if (ok && r.has_stream) {
+    ok = dev_ensure(&r.ostream, (size_t)n, a->stream, false);
+    if (ok) launch_gather(r.stream.p, r.ostream.p, perm, 0, n, 1, a->stream);
+  }
+  if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (reorder gather)");
+  // the held-back rows stay buffered, now in (ts, arrival) order
+  const int64_t keep = n - rel;
+  for (int c = 0; c < nc; ++c) {
+    const int w = type_width(sd.attrs[c].type);
+    hipMemcpyAsync(r.col[c].p, (char*)r.out[c].p + rel * w, (size_t)keep * w, hipMemcpyDeviceToDevice, a->stream);
+  }
+  hipMemcpyAsync(r.ts.p, (char*)r.ots.p + rel * 8, (size_t)keep * 8, hipMemcpyDeviceToDevice, a->stream);
+  if (r.has_stream)
+    hipMemcpyAsync(r.stream.p, (char*)r.ostream.p + rel, (size_t)keep, hipMemcpyDeviceToDevice, a->stream);
+  r.n = keep;
+  const int input = r.input;
+  if (keep == 0) r.input = -1;
+  // the released prefix is a device batch in event-time order
+  const void* cols[kMaxCols];
+  for (int c = 0; c < nc; ++c) cols[c] = r.out[c].p;
+  cep_batch bb{};
+  bb.n = rel;
+  bb.ts = (const int64_t*)r.ots.p;
+  bb.stream = r.has_stream ? (const uint8_t*)r.ostream.p : nullptr;
+  bb.input = input;
+  bb.ncols = nc;
+  bb.cols = cols;
+  bb.on_device = 1;
+  a->last_ts = r.released_max;   // the kernel's order check spans the watermark
+  const int64_t rmax = hb[2];
+  int rc = cep_send_batch(a, &bb);
+  if (rc == CEP_OK) r.released_max = rmax;
+  // the sorted batch buffers are reused by the next watermark: finish first
+  hipStreamSynchronize(a->stream);
   return rc;
 }
 

@@ -264,6 +264,13 @@ void launch_route_collect(const RouteArgs& a, int64_t ntiles, uint32_t* toffs,
                           unsigned long long* dcount, uint64_t* out, hipStream_t s);
 void launch_cf_route(const CfRouteArgs& a, int64_t ntiles, hipStream_t s);
 void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s);
+// event-time reorder (reorder.hip)
+size_t reorder_temp_bytes(int64_t n);
+int reorder_sort(void* temp, size_t temp_bytes, const int64_t* keys_in, int64_t* keys_out, int32_t* idx_in,
+                 int32_t* idx_out, int64_t n, hipStream_t s);
+void launch_upper_bound(const int64_t* sorted, int64_t n, int64_t wm, int64_t* out3, hipStream_t s);
+void launch_gather(const void* src, void* dst, const int32_t* perm, int64_t first, int64_t n, int width,
+                   hipStream_t s);
 void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
                      int64_t rate, int64_t t0, int single_stream, int32_t* key,
                      int64_t* ts, uint8_t* stream, int32_t* id, double* price,

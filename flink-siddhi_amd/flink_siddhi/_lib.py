@@ -134,6 +134,9 @@ SIGNATURES = {
     "cep_input": (C.c_int, [C.c_void_p, C.c_char_p]),
     "cep_set_callback": (C.c_int, [C.c_void_p, C.c_char_p, EMIT_FN, C.c_void_p]),
     "cep_send_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch)]),
+    "cep_buffer_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch)]),
+    "cep_watermark": (C.c_int, [C.c_void_p, C.c_int64]),
+    "cep_buffered": (C.c_int64, [C.c_void_p]),
     "cep_flush": (C.c_int, [C.c_void_p]),
     "cep_output_device": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(cep_rows)]),
     "cep_reset_output": (C.c_int, [C.c_void_p]),

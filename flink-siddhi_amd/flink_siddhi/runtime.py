@@ -166,6 +166,27 @@ class SiddhiAppRuntime:
         device-resident.  `streams` (uint8 per row: input handles) mixes
         several identically-defined streams in one batch.
         """
+        self._send(self._lib.cep_send_batch, stream_id, ts, cols, streams)
+
+    def process_elements(self, stream_id: str, ts, cols: Sequence, streams=None):
+        """Event-time input in any timestamp order: the rows are buffered on
+        the device until a watermark releases them, as the operator's
+        processElement offers records to its PriorityQueue
+        (AbstractSiddhiOperator.java:222-231).  Same arguments as send()."""
+        self._send(self._lib.cep_buffer_batch, stream_id, ts, cols, streams)
+
+    def process_watermark(self, mark: int):
+        """processWatermark (AbstractSiddhiOperator.java:238-247): buffered rows
+        with ts <= mark reach the engine in (ts, arrival) order; later rows
+        stay buffered.  A row older than one already released raises
+        ValueError (late event)."""
+        self._check(self._lib.cep_watermark(self._h, int(mark)))
+
+    def buffered(self) -> int:
+        """Rows waiting for a watermark (the PriorityQueue's size)."""
+        return int(self._lib.cep_buffered(self._h))
+
+    def _send(self, fn, stream_id: str, ts, cols: Sequence, streams=None):
         h = self.input_handle(stream_id)
         defs = self.stream_definition(stream_id)
         on_device = _is_device(ts)
@@ -186,7 +207,7 @@ class SiddhiAppRuntime:
                         cols=ptrs, on_device=1 if on_device else 0)
         if on_device:
             self._wait_producer(ts)
-        self._check(self._lib.cep_send_batch(self._h, C.byref(b)))
+        self._check(fn(self._h, C.byref(b)))
 
     def _wait_producer(self, t):
         """Order the engine's stream after torch's current stream (device

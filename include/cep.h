@@ -170,6 +170,23 @@ int cep_set_callback(cep_app* app, const char* out_id, cep_emit_fn fn,
 /* A batch of InputHandler.send(ts, row) calls — AbstractSiddhiOperator.java:130 */
 int cep_send_batch(cep_app* app, const cep_batch* batch);
 
+/* Event-time mode.  processElement — AbstractSiddhiOperator.java:222-231
+ * (offer to the PriorityQueue<StreamRecord>): buffer rows in any timestamp
+ * order on the device; nothing reaches the engine yet.  All rows buffered
+ * between two watermarks share one input layout (`input`, stream column
+ * present or not). */
+int cep_buffer_batch(cep_app* app, const cep_batch* batch);
+
+/* processWatermark(mark) — AbstractSiddhiOperator.java:238-247: the buffered
+ * rows with ts <= mark go to the engine in (ts, arrival) order (one stable
+ * device sort; the reference PQ orders by ts only, StreamRecordComparator.java:
+ * 32-40); later rows stay buffered.  A row older than one already released
+ * (a late event) is refused with CEP_E_ARG: `within` needs event-time order. */
+int cep_watermark(cep_app* app, int64_t mark);
+
+/* Rows still buffered (the PriorityQueue's size). */
+int64_t cep_buffered(cep_app* app);
+
 /* Deliver every match of the input sent so far to the callbacks; called
  * before emitWatermark / snapshotState / close (AbstractSiddhiOperator.java:246,331,316). */
 int cep_flush(cep_app* app);

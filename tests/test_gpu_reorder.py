@@ -1,0 +1,133 @@
+"""Event-time reorder on the device vs the oracle.
+
+The operator buffers event-time records in a PriorityQueue and hands those
+with ts <= watermark to Siddhi in timestamp order
+(AbstractSiddhiOperator.java:222-231, 238-247).  process_elements /
+process_watermark do the same on the device; ties keep arrival order (the
+reference PQ is not stable — SURVEY.md App. B a5 — so the oracle is fed the
+stable (ts, arrival) order).  Bit-exact against the oracle run on that order.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_same_rows, engine_rows, oracle_run, workload_events
+
+pytestmark = pytest.mark.gpu
+
+import flink_siddhi as fs  # noqa: E402
+from flink_siddhi import workload  # noqa: E402
+
+COLS = ("k", "ts", "id", "price", "stream")
+
+
+def disordered(n, keys, rate, jitter, seed):
+    """The generator stream, arriving out of order: row i arrives at rank of
+    i + U[0, jitter) (bounded lateness)."""
+    w = workload.generate(0, n, keys, rate=rate)
+    rng = np.random.default_rng(seed)
+    arrival = np.argsort(np.arange(n) + rng.integers(0, jitter, n), kind="stable")
+    return {c: w[c][arrival] for c in COLS}
+
+
+def sorted_by_ts(w):
+    o = np.argsort(w["ts"], kind="stable")   # (ts, arrival)
+    return {c: w[c][o] for c in COLS}
+
+
+def run_reorder(plan, w, batches, out="O", perfect_watermarks=True, **opts):
+    rt = fs.SiddhiAppRuntime(plan, **opts)
+    rt.add_callback(out)
+    n = len(w["ts"])
+    cuts = np.linspace(0, n, batches + 1).astype(int)
+    # perfect watermark after batch b: every row not yet arrived is later
+    suffix_min = np.minimum.accumulate(w["ts"][::-1])[::-1]
+    for b in range(batches):
+        s, e = cuts[b], cuts[b + 1]
+        rt.process_elements("A", w["ts"][s:e], [w["k"][s:e], w["ts"][s:e], w["id"][s:e], w["price"][s:e]],
+                            streams=w["stream"][s:e])
+        if perfect_watermarks and e < n:
+            rt.process_watermark(int(suffix_min[e]) - 1)
+    rt.process_watermark(int(w["ts"].max()))
+    assert rt.buffered() == 0
+    rt.flush()
+    got = engine_rows(rt.collect(out))
+    rt.shutdown()
+    return got
+
+
+@pytest.mark.parametrize("rate,batches", [(1, 1), (4, 7), (16, 13)])
+def test_reordered_pattern_matches_oracle_in_event_time_order(rate, batches):
+    w = disordered(40000, 4096, rate, jitter=700, seed=rate)
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(sorted_by_ts(w))).get("O", [])
+    got = run_reorder(workload.PATTERN_PLAN, w, batches)
+    assert_same_rows(got, want, "reorder rate=%d batches=%d" % (rate, batches))
+    assert len(want) > 100
+
+
+def test_reordered_multi_chunk_buffers_across_watermarks():
+    # several engine chunks per release, rows held back over many watermarks
+    w = disordered(120000, 4096, 8, jitter=5000, seed=7)
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(sorted_by_ts(w))).get("O", [])
+    got = run_reorder(workload.PATTERN_PLAN, w, 11, chunk_events=1 << 15)
+    assert_same_rows(got, want, "reorder multi-chunk")
+
+
+def test_watermark_releases_only_rows_at_or_before_it():
+    w = sorted_by_ts(disordered(5000, 2048, 1, jitter=50, seed=3))
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt.add_callback("O")
+    rt.process_elements("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
+    assert rt.buffered() == 5000
+    mid = int(w["ts"][2499])
+    rt.process_watermark(mid)
+    assert rt.buffered() == int((w["ts"] > mid).sum())
+    rt.process_watermark(int(w["ts"][0]) - 1)   # nothing new to release
+    assert rt.buffered() == int((w["ts"] > mid).sum())
+    rt.process_watermark(int(w["ts"].max()))
+    assert rt.buffered() == 0
+    rt.flush()
+    got = engine_rows(rt.collect("O"))
+    rt.shutdown()
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(w)).get("O", [])
+    assert_same_rows(got, want, "watermark split")
+
+
+def test_late_event_is_refused():
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    ts = np.arange(1000, 1100, dtype=np.int64)
+    z = np.zeros(100, dtype=np.int32)
+    p = np.full(100, 0.75)
+    st = np.zeros(100, dtype=np.uint8)
+    rt.process_elements("A", ts, [z, ts, z, p], streams=st)
+    rt.process_watermark(1050)
+    late = np.array([1020], dtype=np.int64)
+    rt.process_elements("A", late, [z[:1], late, z[:1], p[:1]], streams=st[:1])
+    with pytest.raises(ValueError):
+        rt.process_watermark(2000)
+    rt.shutdown()
+
+
+def test_reordered_filter_matches_oracle():
+    plan = workload.FILTER_PLAN
+    n = 30000
+    w = workload.generate(0, n, 1, single_stream=True, rate=4)
+    rng = np.random.default_rng(11)
+    arrival = np.argsort(np.arange(n) + rng.integers(0, 300, n), kind="stable")
+    cols = {c: w[c][arrival] for c in ("id", "price", "ts")}
+    rt = fs.SiddhiAppRuntime(plan)
+    rt.add_callback("O")
+    name = rt.intern("test_event")
+    names = np.full(n, name, np.int32)
+    for s in range(0, n, 7000):
+        e = min(n, s + 7000)
+        rt.process_elements("inputStream", cols["ts"][s:e],
+                            [cols["id"][s:e], names[s:e], cols["price"][s:e], cols["ts"][s:e]])
+    rt.process_watermark(int(cols["ts"].max()))
+    rt.flush()
+    got = engine_rows(rt.collect("O"))
+    rt.shutdown()
+    o = np.argsort(cols["ts"], kind="stable")
+    ev = [("inputStream", t, (i, name, p, t)) for i, p, t in
+          zip(cols["id"][o].tolist(), cols["price"][o].tolist(), cols["ts"][o].tolist())]
+    want = oracle_run(plan, ev)["O"]
+    assert_same_rows(got, want, "reordered filter")
