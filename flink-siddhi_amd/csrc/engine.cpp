@@ -134,6 +134,7 @@ struct cep_app {
   int64_t last_ts = INT64_MIN;
   int64_t launches[16] = {0};
   double kernel_ms[16] = {0};
+  int64_t kernel_timed[16] = {0};
   std::vector<TimedLaunch> timed;
   std::vector<hipEvent_t> event_pool;
   std::vector<std::unique_ptr<char[]>> name_store;
@@ -168,16 +169,19 @@ struct LaunchTimer {
   int kind;
   hipStream_t st;
   hipEvent_t s = nullptr;
+  // profile = k: HIP events around every k-th launch of each kernel kind
+  // (each event between two kernels widens the gap between them by ~5 us)
   LaunchTimer(cep_app* app, int k, hipStream_t on = nullptr)
       : a(app), kind(k), st(on ? on : app->stream) {
+    const bool timed = a->opt.profile > 0 && a->launches[k] % a->opt.profile == 0;
     a->launches[k]++;
-    if (a->opt.profile) {
+    if (timed) {
       s = pool_event(a);
       hipEventRecord(s, st);
     }
   }
   ~LaunchTimer() {
-    if (a->opt.profile) {
+    if (s) {
       hipEvent_t e = pool_event(a);
       hipEventRecord(e, st);
       a->timed.push_back({kind, s, e});
@@ -190,6 +194,7 @@ void harvest_timers(cep_app* a) {
     float ms = 0;
     hipEventElapsedTime(&ms, t.a, t.b);
     a->kernel_ms[t.kind] += ms;
+    a->kernel_timed[t.kind]++;
     a->event_pool.push_back(t.a);
     a->event_pool.push_back(t.b);
   }
@@ -536,14 +541,18 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
                    const RowsArgs& rows_all, const CfPlan& cf,
                    const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
   const int P = 1 << rt.pa.buckets_log2;
-  hipEventRecord(a->in_ready, a->stream);
-  hipStreamWaitEvent(a->side, a->in_ready, 0);
   // Both passes on the main stream by default: k_cfpart and k_cfwalk cannot
   // share a CU (each fills its register file), so the side stream only
   // time-slices them (measured: no throughput gain, inflated kernel times).
-  // CEP_OVERLAP=1 puts the partition on the side stream.
+  // CEP_OVERLAP=1 puts the partition on the side stream.  Serial mode issues
+  // no cross-stream events: every event between two kernels of one stream
+  // costs a gap (rocprofv3 trace: ~15 us between k_cfpart and k_cfwalk).
   static const bool overlap = std::getenv("CEP_OVERLAP") != nullptr;
   hipStream_t side = overlap ? a->side : a->stream;
+  if (overlap) {
+    hipEventRecord(a->in_ready, a->stream);
+    hipStreamWaitEvent(a->side, a->in_ready, 0);
+  }
   for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.cf_chunk) {
     const int b = rt.cur;
     rt.cur ^= 1;
@@ -569,13 +578,15 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     pa.ntiles = (int32_t)ntiles;
     pa.err = (unsigned int*)a->err.p;
     if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
-    if (rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
+    if (overlap && rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
     {
       LaunchTimer t(a, CEP_K_CF_PARTITION, side);
       launch_cf_partition(pa, ntiles, side);
     }
-    hipEventRecord(rt.part_done[b], side);
-    hipStreamWaitEvent(a->stream, rt.part_done[b], 0);
+    if (overlap) {
+      hipEventRecord(rt.part_done[b], side);
+      hipStreamWaitEvent(a->stream, rt.part_done[b], 0);
+    }
     CfWalkArgs wa{};
     wa.pat = rt.pa;
     wa.cf = cf;
@@ -600,7 +611,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       LaunchTimer t(a, CEP_K_CF_WALK);
       launch_cf_walk(wa, P, a->stream);
     }
-    hipEventRecord(rt.walk_done[b], a->stream);
+    if (overlap) hipEventRecord(rt.walk_done[b], a->stream);
     rt.used[b] = true;
   }
   return CEP_OK;
@@ -1253,6 +1264,7 @@ int cep_stats(cep_app* a, cep_stats_t* s) {
   for (int i = 0; i < 16; ++i) {
     s->kernel_launches[i] = a->launches[i];
     s->kernel_ms[i] = a->kernel_ms[i];
+    s->kernel_timed[i] = a->kernel_timed[i];
   }
   return CEP_OK;
 }

@@ -114,7 +114,7 @@ class cep_rows(C.Structure):
 class cep_stats_t(C.Structure):
     _fields_ = [("events_in", C.c_int64), ("matches_out", C.c_int64),
                 ("batches", C.c_int64), ("kernel_launches", C.c_int64 * 16),
-                ("kernel_ms", C.c_double * 16)]
+                ("kernel_ms", C.c_double * 16), ("kernel_timed", C.c_int64 * 16)]
 
 
 EMIT_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(cep_rows))

@@ -80,7 +80,7 @@ typedef struct cep_options {
   int64_t key_capacity;    /* partition / group keys are ints in [0, key_capacity) (default 1<<20) */
   int64_t chunk_events;    /* events per device chunk (default 1<<22) */
   int32_t buckets_log2;    /* key buckets per chunk, log2 (default 10) */
-  int32_t profile;         /* 1: time every kernel with HIP events (cep_stats) */
+  int32_t profile;         /* k >= 1: time every k-th launch of each kernel with HIP events (cep_stats) */
   int32_t ordered_output;  /* 1: deliver matches in Siddhi's global emission
                               order; 0: per-key order (default 1) */
   int32_t key_stride;      /* multi-GPU: this shard owns keys with key % key_stride == key_offset (default 1/0) */
@@ -126,6 +126,7 @@ typedef struct {
   int64_t batches;
   int64_t kernel_launches[16];
   double kernel_ms[16];       /* with cep_options.profile: summed HIP-event time */
+  int64_t kernel_timed[16];   /* launches kernel_ms covers (profile = k: every k-th) */
 } cep_stats_t;
 
 /* Kernel kinds indexing cep_stats_t arrays. */
