@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--events", type=int, default=0, help="events per step per GPU")
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--rate", type=int, default=400, help="events per ms")
-    ap.add_argument("--chunk", type=int, default=1 << 24)
+    ap.add_argument("--chunk", type=int, default=1 << 25)
     ap.add_argument("--buckets-log2", type=int, default=0,
                     help="key buckets = 2^n (0: engine default, <= 512 keys per bucket)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

@@ -648,29 +648,31 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
   const uint16_t* rhi = rlo + ntiles;
   const int tb = tid * TPT;
-  uint32_t lop[TPT / 2];   // packed u16 segment starts of tiles tid*TPT + i
-  uint32_t ys[TPT / 2];    // packed u16 segment ends
-  if ((ntiles & (TPT - 1)) == 0 && tb + TPT <= ntiles) {
-    // TPT u16 per row: one 8- or 16-byte load per row
-    if constexpr (TPT == 8) {
-      const uint4 x = *(const uint4*)(rlo + tb), y = *(const uint4*)(rhi + tb);
-      lop[0] = x.x; lop[1 % (TPT / 2)] = x.y; lop[2 % (TPT / 2)] = x.z; lop[3 % (TPT / 2)] = x.w;
-      ys[0] = y.x; ys[1 % (TPT / 2)] = y.y; ys[2 % (TPT / 2)] = y.z; ys[3 % (TPT / 2)] = y.w;
+  // packed u16 offsets of tiles tid*TPT + i in one row of the bucket-major
+  // table: one 8- or 16-byte load when the row is whole, else per tile
+  auto load_tile_off = [&](const uint16_t* row, uint32_t (&o)[TPT / 2]) {
+    if ((ntiles & (TPT - 1)) == 0 && tb + TPT <= ntiles) {
+      if constexpr (TPT == 8) {
+        const uint4 x = *(const uint4*)(row + tb);
+        o[0] = x.x; o[1 % (TPT / 2)] = x.y; o[2 % (TPT / 2)] = x.z; o[3 % (TPT / 2)] = x.w;
+      } else {
+        const uint2 x = *(const uint2*)(row + tb);
+        o[0] = x.x; o[1 % (TPT / 2)] = x.y;
+      }
     } else {
-      const uint2 x = *(const uint2*)(rlo + tb), y = *(const uint2*)(rhi + tb);
-      lop[0] = x.x; lop[1 % (TPT / 2)] = x.y;
-      ys[0] = y.x; ys[1 % (TPT / 2)] = y.y;
-    }
-  } else {
 #pragma unroll
-    for (int i = 0; i < TPT / 2; ++i) lop[i] = ys[i] = 0;
+      for (int i = 0; i < TPT / 2; ++i) o[i] = 0;
 #pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      const int t = tb + i;
-      lop[i >> 1] |= (t < ntiles ? (uint32_t)rlo[t] : 0u) << (16 * (i & 1));
-      ys[i >> 1] |= (t < ntiles ? (uint32_t)rhi[t] : 0u) << (16 * (i & 1));
+      for (int i = 0; i < TPT; ++i) {
+        const int t = tb + i;
+        o[i >> 1] |= (t < ntiles ? (uint32_t)row[t] : 0u) << (16 * (i & 1));
+      }
     }
-  }
+  };
+  uint32_t lop[TPT / 2];   // packed u16 segment starts (prefix phase only)
+  uint32_t ys[TPT / 2];    // packed u16 segment ends
+  load_tile_off(rlo, lop);
+  load_tile_off(rhi, ys);
 
   int n = (int)(hdr & 0xffu);
   // Slots 0 / 1 (ts + captures) live in registers for the whole kernel: read
@@ -793,6 +795,10 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     } else {
       nw = L.seg[t1] - L.seg[t0];
       const uint32_t wb = L.seg[t0];
+      // this thread's segment starts, re-read (L2) per window rather than
+      // held in registers across the whole walk
+      uint32_t lop[TPT / 2];
+      load_tile_off(rlo, lop);
 #pragma unroll
       for (int i = 0; i < TPT; ++i) {
         const int t = tid * TPT + i;

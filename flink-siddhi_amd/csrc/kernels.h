@@ -197,7 +197,7 @@ constexpr int kCfTile = CF_TILE_ROWS;                  // rows per tile
 constexpr int kCfWalkThreads = 512;
 constexpr int kCfWindow = 2048;                        // records per LDS window (nw <= 1)
 constexpr int kCfMaxKeys = 512;                        // keys per bucket
-constexpr int kCfMaxTiles = (16 << 20) / kCfTile;      // chunk <= 16 Mi rows
+constexpr int kCfMaxTiles = (32 << 20) / kCfTile;      // chunk <= 32 Mi rows
 constexpr int kCfMaxBuckets = 4096;
 constexpr int kCfMaxCaps = 2;                          // captured words per pending slot
 
