@@ -6,3 +6,9 @@ mkdir -p gpurun_out
 CEP_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --events 16777216 --steps 2 --warmup 1 \
   --no-cpu > gpurun_out/multi_rehearsal.log 2>&1
+rc=$?
+[ $rc -ne 0 ] && { tail -20 gpurun_out/multi_rehearsal.log; exit $rc; }
+CEP_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --events 16777216 --steps 2 --warmup 1 \
+  --no-cpu --ingest prepartitioned > gpurun_out/multi_rehearsal_pre.log 2>&1 || { tail -20 gpurun_out/multi_rehearsal_pre.log; exit 1; }
+grep -h '^{' gpurun_out/multi_rehearsal.log gpurun_out/multi_rehearsal_pre.log | cut -c1-400
