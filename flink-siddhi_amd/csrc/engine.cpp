@@ -1298,7 +1298,7 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
   };
   const char magic[4] = {'C', 'E', 'P', 'S'};
   put(magic, 4);
-  uint32_t ver = 2;
+  uint32_t ver = 3;   // 3: + the event-time reorder buffer
   put(&ver, 4);
   uint64_t h = plan_hash(a->app);
   put(&h, 8);
@@ -1330,6 +1330,29 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
         for (uint32_t w = 0; w < sw; ++w) put(&slots[((size_t)j * sw + w) * ks + i], 8);
     }
   }
+  // rows waiting for a watermark (the operator checkpoints its PriorityQueue
+  // as "queuedRecordsState": AbstractSiddhiOperator.java:98, 396-404)
+  {
+    const auto& r = a->ro;
+    const int32_t in = r.n > 0 ? r.input : -1;
+    const uint8_t hs = r.has_stream ? 1 : 0;
+    put(&in, 4);
+    put(&hs, 1);
+    put(&r.n, 8);
+    put(&r.released_max, 8);
+    if (r.n > 0) {
+      const StreamSchema& sd = a->app.inputs[r.input];
+      std::vector<uint8_t> tmp;
+      auto pull = [&](const DevBuf& b, size_t bytes) {
+        tmp.resize(bytes);
+        hipMemcpy(tmp.data(), b.p, bytes, hipMemcpyDeviceToHost);
+        put(tmp.data(), bytes);
+      };
+      for (size_t c = 0; c < sd.attrs.size(); ++c) pull(r.col[c], (size_t)r.n * type_width(sd.attrs[c].type));
+      pull(r.ts, (size_t)r.n * 8);
+      if (r.has_stream) pull(r.stream, (size_t)r.n);
+    }
+  }
   *buf = (uint8_t*)std::malloc(out.size());
   if (!*buf) return fail(a, CEP_E_DEVICE, "out of host memory");
   std::memcpy(*buf, out.data(), out.size());
@@ -1351,7 +1374,7 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   uint64_t h;
   int64_t ev;
   uint32_t np;
-  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver != 2 || !get(&h, 8) ||
+  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || (ver != 2 && ver != 3) || !get(&h, 8) ||
       !get(&ev, 8) || !get(&np, 4))
     return fail(a, CEP_E_STATE, "not a libcep snapshot");
   if (h != plan_hash(a->app) || np != a->pats.size())
@@ -1384,6 +1407,37 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     }
     hipMemcpy(rt.khdr.p, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice);
     hipMemcpy(rt.kslot.p, slots.data(), slots.size() * 8, hipMemcpyHostToDevice);
+  }
+  auto& r = a->ro;
+  r.n = 0;
+  r.input = -1;
+  r.released_max = INT64_MIN;
+  if (ver >= 3) {
+    int32_t in;
+    uint8_t hs;
+    int64_t n, rmax;
+    if (!get(&in, 4) || !get(&hs, 1) || !get(&n, 8) || !get(&rmax, 8) || n < 0 ||
+        (n > 0 && (in < 0 || in >= (int)a->app.inputs.size())))
+      return fail(a, CEP_E_STATE, "corrupt snapshot (reorder buffer)");
+    r.released_max = rmax;
+    if (n > 0) {
+      const StreamSchema& sd = a->app.inputs[in];
+      auto push = [&](DevBuf* b, size_t bytes) -> bool {
+        if (off + bytes > len || !dev_ensure(b, bytes, a->stream, false)) return false;
+        hipMemcpy(b->p, buf + off, bytes, hipMemcpyHostToDevice);
+        off += bytes;
+        return true;
+      };
+      bool ok = true;
+      for (size_t c = 0; c < sd.attrs.size() && ok; ++c)
+        ok = push(&r.col[c], (size_t)n * type_width(sd.attrs[c].type));
+      ok = ok && push(&r.ts, (size_t)n * 8);
+      if (hs) ok = ok && push(&r.stream, (size_t)n);
+      if (!ok) return fail(a, CEP_E_STATE, "truncated snapshot (reorder buffer)");
+      r.input = in;
+      r.has_stream = hs != 0;
+      r.n = n;
+    }
   }
   a->events_in = ev;
   return CEP_OK;

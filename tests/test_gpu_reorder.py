@@ -131,3 +131,34 @@ def test_reordered_filter_matches_oracle():
           zip(cols["id"][o].tolist(), cols["price"][o].tolist(), cols["ts"][o].tolist())]
     want = oracle_run(plan, ev)["O"]
     assert_same_rows(got, want, "reordered filter")
+
+
+def test_snapshot_keeps_rows_waiting_for_a_watermark():
+    # the operator checkpoints its queue ("queuedRecordsState",
+    # AbstractSiddhiOperator.java:98): buffered rows survive snapshot / restore
+    w = disordered(40000, 4096, 2, jitter=900, seed=5)
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(sorted_by_ts(w))).get("O", [])
+    half = 23000
+    suffix_min = np.minimum.accumulate(w["ts"][::-1])[::-1]
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt.add_callback("O")
+    rt.process_elements("A", w["ts"][:half], [w["k"][:half], w["ts"][:half], w["id"][:half], w["price"][:half]],
+                        streams=w["stream"][:half])
+    rt.process_watermark(int(suffix_min[half]) - 1)
+    held = rt.buffered()
+    assert held > 0
+    rt.flush()
+    first = engine_rows(rt.collect("O"))
+    snap = rt.snapshot()
+    rt.shutdown()
+    rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt2.add_callback("O")
+    rt2.restore(snap)
+    assert rt2.buffered() == held
+    rt2.process_elements("A", w["ts"][half:], [w["k"][half:], w["ts"][half:], w["id"][half:], w["price"][half:]],
+                         streams=w["stream"][half:])
+    rt2.process_watermark(int(w["ts"].max()))
+    rt2.flush()
+    second = engine_rows(rt2.collect("O"))
+    rt2.shutdown()
+    assert_same_rows(first + second, want, "reorder snapshot/restore")
