@@ -13,12 +13,19 @@ the keys k % N == rank and processes N events per step (weak scaling).
 `--workload filter` runs configs[1] (config 2): `inputStream[price > 0.5 and
 id % 7 == 0] select *` over 10^8 events.
 
+Before the timed region (N=1): a parity check — a fresh runtime processes the
+first step's events and the order-sensitive digest of its device output is
+compared with oracle/cep_oracle.c's digest over the same events ("parity" in
+the JSON line) — and the CPU baseline (the same restatement sharded by key
+over the host's cores).
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -32,10 +39,13 @@ sys.path.insert(0, str(ROOT / "flink-siddhi_amd"))
 # timing every launch costs ~4 % of the throughput; CEP_PROFILE=0: none)
 PROFILE_EVERY = int(os.environ.get("CEP_PROFILE", "4"))
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
-PATTERN_IN_BYTES = 4 + 8 + 1 + 4 + 8     # k, ts, stream, id, price per event
-PATTERN_OUT_BYTES = 4 + 8 + 8 + 8 + 8    # k, p1, p2, t + event ts per match
+PATTERN_IN_BYTES = 4 + 8 + 1 + 4 + 8     # k, ts, stream, id, price per event (SURVEY §8d)
+PATTERN_SEL_BYTES = 4 + 8 + 8 + 8         # k, p1, p2, t per match (28 B)
+PATTERN_OUT_BYTES = PATTERN_SEL_BYTES + 8 + 8   # + event ts + arrival seq the engine writes
+CF_REC_BYTES = 16                         # closed-form record (w0 + one carried word)
+CF_STATE_BYTES = 2 * (4 + 16)             # per key per walk launch: header + slot 0 (ts, p1), read + write
 FILTER_IN_BYTES = 4 + 8                   # id, price per event
-FILTER_OUT_BYTES = 4 + 4 + 8 + 8 + 8      # id, name, price, timestamp + event ts
+FILTER_OUT_BYTES = 4 + 4 + 8 + 8 + 8 + 8  # id, name, price, timestamp + event ts + seq
 
 
 def parse():
@@ -50,8 +60,8 @@ def parse():
     ap.add_argument("--chunk", type=int, default=1 << 25)
     ap.add_argument("--buckets-log2", type=int, default=0,
                     help="key buckets = 2^n (0: engine default, <= 512 keys per bucket)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity check")
     ap.add_argument("--ingest", choices=["shuffle", "prepartitioned"], default="shuffle",
                     help="multi-GPU pattern input: engine key shuffle over RCCL, or keyed upstream")
     return ap.parse_args()
@@ -89,132 +99,160 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(world, v: float) -> float:
+def reduce_over_ranks(world, v: float, op: str) -> float:
     if world == 1:
         return v
     import torch
     import torch.distributed as dist
     t = torch.tensor([v], dtype=torch.float64, device=_coll_device())
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
 
 
-def sum_over_ranks(world, v: float) -> float:
-    if world == 1:
-        return v
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device=_coll_device())
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+def host_cores():
+    """Host cores this process may use: the CPU affinity set, capped by the
+    cgroup CPU quota when one is set (a GPU box's share of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, p = open(f).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            quota = q / p
+    except (OSError, ValueError):
+        pass
+    use = n if quota is None else max(1, min(n, int(math.ceil(quota))))
+    return use, n, quota
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (scripts/gpu_pmc.sh -> scripts/pmc_summary.py -> profiles/r01_pmc.json;
-    FETCH_SIZE doubled per the gfx950 caveat).  Measured in separate
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (scripts/gpu_pmc.sh -> scripts/pmc_summary.py -> profiles/rNN_pmc.json;
+    FETCH_SIZE doubled per the gfx950 caveat), measured in separate
     rocprofv3 --pmc passes of this same bench command; null if absent."""
     import glob
-    import json as _json
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                          "profiles", "*pmc*.json")))
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*pmc*.json")))
     for f in reversed(files):
         try:
-            d = _json.load(open(f))
+            d = json.load(open(f))
         except (OSError, ValueError):
             continue
         if kernel in d and "hbm_bytes_per_launch" in d[kernel]:
             return {"bytes_per_launch": round(d[kernel]["hbm_bytes_per_launch"]),
                     "read": round(d[kernel]["hbm_read_bytes"]),
                     "write": round(d[kernel]["hbm_write_bytes"]),
-                    "source": os.path.relpath(f, os.path.dirname(os.path.abspath(__file__)))}
+                    "source": os.path.relpath(f, str(ROOT))}
     return None
 
 
-def cpu_baseline_pattern(args, budget_s):
-    """Oracle C restatement (kind "port") on the host cores: one thread over a
-    bounded prefix of the stream (~0.8 x budget_s of CPU time), then the same
-    restatement sharded by key (key % T, arrival order kept per shard) over T
-    threads (ctypes releases the GIL), timed over one pre-split sample of up
-    to 2^27 events.  Reported value = the T-thread rate; the 1-thread rate is
-    kept beside it."""
-    import threading
+# ---------------------------------------------------------------- pattern --
+def pattern_conds():
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cep_oracle as CO
+    return CO, CO.cond(("price", 0, ">", 0.5)), CO.cond(("id", 7, "==", 0))
+
+
+def pattern_parity(args, n, opts):
+    """Fresh runtime over the first step's events (events [0, n), the bench
+    geometry): the order-sensitive digest of its device output vs the C
+    restatement's digest over the same events, sharded by key over the host
+    threads.  Returns (result dict, host columns for the CPU baseline)."""
+    import torch
+    import flink_siddhi as fs
+    from flink_siddhi import workload
+    CO, f, g = pattern_conds()
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, **dict(opts, profile=0))
+    d = workload.generate_device(0, n, args.keys, rate=args.rate)
+    rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
+    _, seq, cols = rt.output_tensors("O", copy=False)
+    got_m = int(seq.shape[0])
+    got_d = workload.rows_digest(cols[0], cols[1], cols[2], cols[3], seq)
+    rt.flush()
+    rt.shutdown()
+    del d, seq, cols
+    torch.cuda.empty_cache()
+    T, _, _ = host_cores()
+    w = CO.generate(0, n, args.keys, rate=args.rate, threads=T)
+    want_m, want_d, _ = CO.pattern_mt(w, args.keys, f, g, True, 10000, threads=T)
+    kept = float(((w["stream"] == 0) & (w["price"] > 0.5)).sum() +
+                 ((w["stream"] == 1) & (w["id"] % 7 == 0)).sum()) / n
+    res = {"parity": "ok" if (got_m, got_d) == (want_m, want_d) else "MISMATCH",
+           "events": n, "matches": got_m, "digest": "%016x" % got_d,
+           "oracle_matches": want_m, "oracle_digest": "%016x" % want_d,
+           "checker": "oracle/cep_oracle.c oracle_pattern_mt (fresh state, events [0, n))"}
+    return res, w, kept
+
+
+def cpu_baseline_pattern(args, w):
+    """The C restatement (kind "port": the Java reference cannot run in this
+    image) on the host cores: one thread, then sharded by key
+    (k % T) over T threads, over the same 2^28 events of the parity check."""
+    CO, f, g = pattern_conds()
+    n = len(w["ts"])
+    T, naff, quota = host_cores()
+    m1, _, s1 = CO.pattern_mt(w, args.keys, f, g, True, 10000, threads=1)
+    mT, _, sT = CO.pattern_mt(w, args.keys, f, g, True, 10000, threads=T)
+    return {"value": round(n / sT, 1), "unit": "events/s", "cores": T, "kind": "port",
+            "sample": "events [0, %d) of the config-3 stream (K=%d, R=%d/ms), oracle/cep_oracle.c "
+                      "sharded by key over %d threads (affinity %d CPUs, cgroup quota %s), %d matches, "
+                      "%.2f s; 1 thread: %.0f events/s (%.2f s)"
+                      % (n, args.keys, args.rate, T, naff, "none" if quota is None else "%.1f" % quota,
+                         mT, sT, n / s1, s1),
+            "value_1core": round(n / s1, 1)}
+
+
+# ----------------------------------------------------------------- filter --
+def filter_parity(args, n):
     import numpy as np
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import cep_oracle as CO
+    import torch
+    import flink_siddhi as fs
     from flink_siddhi import workload
-    f, g = CO.cond(("price", 0, ">", 0.5)), CO.cond(("id", 7, "==", 0))
-    # one thread
-    po = CO.PatternOracle(args.keys, f, g, every=True, within=10000)
-    chunk = 1 << 22
-    done, spent, matches = 0, 0.0, 0
-    while spent < budget_s * 0.8 and done < (1 << 28):
-        w = workload.generate(done, chunk, args.keys, rate=args.rate)
-        t0 = time.perf_counter()
-        _, _, m = po.run(w, out_cap=chunk)
-        spent += time.perf_counter() - t0
-        matches += m
-        done += chunk
-    one = done / spent
-    # T threads, key-sharded
-    T = max(1, min(16, os.cpu_count() or 1))
-    n = min(1 << 27, int(one * budget_s / 2 * T))
-    n = max(chunk, (n // chunk) * chunk)
-    w = workload.generate(0, n, args.keys, rate=args.rate)
-    shard = w["k"] % T
-    order = np.argsort(shard, kind="stable")
-    bounds = np.searchsorted(shard[order], np.arange(T + 1))
-    parts = []
-    for t in range(T):
-        idx = order[bounds[t]:bounds[t + 1]]
-        part = {c: np.ascontiguousarray(w[c][idx]) for c in ("k", "stream", "id", "price", "ts")}
-        part["k"] = (part["k"] // T).astype(np.int32)   # shard-local dense keys
-        parts.append(part)
-    del w, shard, order
-    oracles = [CO.PatternOracle((args.keys + T - 1) // T, f, g, every=True, within=10000)
-               for _ in range(T)]
-    res = [0] * T
-
-    def work(t):
-        _, _, m = oracles[t].run(parts[t], out_cap=len(parts[t]["ts"]))
-        res[t] = m
-
-    threads = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-    t0 = time.perf_counter()
-    for th in threads:
-        th.start()
-    for th in threads:
-        th.join()
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "events/s", "cores": T, "kind": "port",
-            "sample": "first %d events of the config-3 stream (K=%d, R=%d/ms) sharded by key "
-                      "over %d threads, oracle/cep_oracle.c, %d matches, %.2f s; 1 thread: "
-                      "%.0f events/s over the first %d events"
-                      % (n, args.keys, args.rate, T, sum(res), dt, one, done),
-            "value_1core": one}
+    CO, _, _ = pattern_conds()
+    rt = fs.SiddhiAppRuntime(workload.FILTER_PLAN, ordered_output=0)
+    d = workload.generate_device(0, n, 1, single_stream=True)
+    name = torch.zeros(n, dtype=torch.int32, device="cuda")
+    rt.send("inputStream", d["ts"], [d["id"], name, d["price"], d["ts"]])
+    _, seq, cols = rt.output_tensors("O", copy=False)
+    got_m = int(seq.shape[0])
+    got_d = workload.rows_digest(cols[0], cols[2], cols[2], cols[3], seq)
+    ordered = bool((seq[1:] > seq[:-1]).all().item()) if got_m > 1 else True
+    rt.flush()
+    rt.shutdown()
+    del d, name, seq, cols
+    T, _, _ = host_cores()
+    w = CO.generate(0, n, 1, single_stream=True, threads=T)
+    sel = CO.filter_indices(w["id"], w["price"], CO.cond(("price", 0, ">", 0.5), ("id", 7, "==", 0)))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    want_d = workload.rows_digest(t(w["id"][sel]), t(w["price"][sel]), t(w["price"][sel]),
+                                  t(w["ts"][sel]), t(sel))
+    ok = ordered and (got_m, got_d) == (len(sel), want_d)
+    return {"parity": "ok" if ok else "MISMATCH", "events": n, "matches": got_m,
+            "digest": "%016x" % got_d, "oracle_matches": int(len(sel)), "oracle_digest": "%016x" % want_d,
+            "checker": "oracle/cep_oracle.c oracle_filter (arrival order)"}, w
 
 
-def cpu_baseline_filter(args, n_total, budget_s):
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import cep_oracle as CO
-    from flink_siddhi import workload
+def cpu_baseline_filter(w):
+    CO, _, _ = pattern_conds()
     f = CO.cond(("price", 0, ">", 0.5), ("id", 7, "==", 0))
-    chunk = 1 << 23
-    done, spent = 0, 0.0
-    while spent < budget_s and done < n_total:
-        w = workload.generate(done, chunk, 1, single_stream=True)
-        t0 = time.perf_counter()
-        CO.filter_indices(w["id"], w["price"], f)
-        spent += time.perf_counter() - t0
-        done += chunk
-    return {"value": done / spent, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": "first %d events of the config-2 stream, oracle/cep_oracle.c "
-                      "single-threaded, %.1f s" % (done, spent)}
+    n = len(w["id"])
+    t0 = time.perf_counter()
+    CO.filter_indices(w["id"], w["price"], f)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": "events [0, %d) of the config-2 stream, oracle/cep_oracle.c single-threaded, "
+                      "%.2f s" % (n, dt)}
 
 
+# ------------------------------------------------------------------- main --
 def main():
     args = parse()
-    import numpy as np
     import torch
     import flink_siddhi as fs
     from flink_siddhi import _lib as L
@@ -235,11 +273,24 @@ def main():
     else:
         plan = workload.FILTER_PLAN
         opts = dict(device=local, profile=PROFILE_EVERY, ordered_output=0)
+
+    # parity + CPU baseline first (N=1): the host leg needs the same events
+    parity, cpu, kept = None, None, None
+    if world == 1 and not (args.no_parity and args.no_cpu):
+        if pattern:
+            parity, w, kept = pattern_parity(args, n, opts)
+            if not args.no_cpu:
+                cpu = cpu_baseline_pattern(args, w)
+        else:
+            parity, w = filter_parity(args, n)
+            if not args.no_cpu:
+                cpu = cpu_baseline_filter(w)
+        if args.no_parity:
+            parity = None
+        del w
     rt = fs.SiddhiAppRuntime(plan, **opts)
 
     # Inputs for every step, generated on the device before the timed region.
-    # Multi-GPU: rank r's events are the ones whose key it owns (the result of
-    # the keyBy shuffle), drawn from its own contiguous index ranges.
     # Multi-GPU ingest: "shuffle" (default) — rank r holds global index range
     # r of each step and the engine routes it (push-down + owner = k % world),
     # RCCL all-to-all moves the records, each owner walks what it received;
@@ -289,9 +340,9 @@ def main():
     barrier(world)
     dt = time.perf_counter() - t0
     st1 = rt.stats()
-    dt_max = max_over_ranks(world, dt)
-    events_total = sum_over_ranks(world, float(n * steps))
-    matches_total = sum_over_ranks(world, float(st1.matches_out - st0.matches_out))
+    dt_max = reduce_over_ranks(world, dt, "max")
+    events_total = reduce_over_ranks(world, float(n * steps), "sum")
+    matches_total = reduce_over_ranks(world, float(st1.matches_out - st0.matches_out), "sum")
     value = events_total / dt_max
 
     # per-kernel HIP-event times on the engine's stream over the timed region
@@ -303,41 +354,55 @@ def main():
         ms = st1.kernel_ms[k] - st0.kernel_ms[k]
         if launches and timed and ms > 0:
             kern[name] = {"launches": int(launches), "timed_launches": int(timed),
-                          "avg_us": 1e3 * ms / timed, "total_ms": ms / timed * launches}
+                          "avg_us": round(1e3 * ms / timed, 2), "total_ms": round(ms / timed * launches, 3)}
     m_per_event = (st1.matches_out - st0.matches_out) / float(n * steps)
+    ev_total = float(n * steps)
+    keys_local = (args.keys + world - 1) // world
     if pattern:
-        # a launch of either pattern kernel processes one chunk of events: its
-        # algorithmic bytes are SURVEY §8(d)'s per-event figure x the chunk
-        alg_per_event = PATTERN_IN_BYTES + PATTERN_OUT_BYTES * m_per_event
-        per_launch = {}
-        for kname in ("k_partition", "k_walk", "k_cfpart", "k_cfwalk"):
-            if kname in kern:
-                per_launch[kname] = alg_per_event * n * steps / kern[kname]["launches"]
+        # Pipeline (headline): SURVEY §8(d)'s algorithmic bytes per event —
+        # the 25 B the pattern reads + 28 B per selected match row — over the
+        # whole step.  Per kernel: the bytes each kernel must move in this
+        # design (k_cfpart: input + records; k_cfwalk: records + output rows +
+        # per-key state), per launch.
+        alg_per_event = PATTERN_IN_BYTES + PATTERN_SEL_BYTES * m_per_event
+        kept = kept if kept is not None else 0.33
+        total_bytes = {
+            "k_cfpart": ev_total * (PATTERN_IN_BYTES + CF_REC_BYTES * kept),
+            "k_cfwalk": ev_total * (CF_REC_BYTES * kept + PATTERN_OUT_BYTES * m_per_event),
+            "k_partition": ev_total * PATTERN_IN_BYTES,
+            "k_walk": ev_total * PATTERN_OUT_BYTES * m_per_event,
+        }
+        for k in ("k_cfwalk", "k_walk"):
+            if k in kern:
+                total_bytes[k] += kern[k]["launches"] * keys_local * CF_STATE_BYTES
         if shuffle_mode:
-            # route reads the whole step batch once; the owner's partition pass
-            # then reads records, not events (its bytes are not attributed here)
-            per_launch["k_route"] = PATTERN_IN_BYTES * n
+            total_bytes["k_route"] = ev_total * PATTERN_IN_BYTES
     else:
-        per_launch = {"k_filter": (FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event) * n}
         alg_per_event = FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event
+        total_bytes = {"k_filter": ev_total * alg_per_event}
+    per_kernel = {}
+    for kname, b in total_bytes.items():
+        if kname not in kern:
+            continue
+        per_launch = b / kern[kname]["launches"]
+        ach = per_launch / (kern[kname]["avg_us"] * 1e-6) / 1e9
+        per_kernel[kname] = {"bytes_per_launch": round(per_launch), "avg_launch_us": kern[kname]["avg_us"],
+                             "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                             "traffic": pmc_traffic(kname) if world == 1 else None}
     roofline = None
-    timed_k = [k for k in kern if k in per_launch]
-    if timed_k:   # CEP_PROFILE=0 (no per-kernel timer events): no kernel roofline
-        dom = max(timed_k, key=lambda k: kern[k]["total_ms"])
-        achieved = per_launch[dom] / (kern[dom]["avg_us"] * 1e-6) / 1e9
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": pmc_traffic(dom) if world == 1 else None,
-                    "bytes_per_launch": per_launch[dom], "avg_launch_us": round(kern[dom]["avg_us"], 2)}
+    if per_kernel:   # CEP_PROFILE=0 (no per-kernel timer events): no kernel roofline
+        dom = max(per_kernel, key=lambda k: kern[k]["total_ms"])
+        pk = per_kernel[dom]
+        tr = pk["traffic"]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": pk["achieved"], "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": pk["frac"],
+                    "traffic": tr["bytes_per_launch"] if tr else None,
+                    "bytes_per_launch": pk["bytes_per_launch"], "avg_launch_us": pk["avg_launch_us"]}
     per_gpu_events = value / world
     pipeline = {"alg_bytes_per_event": round(alg_per_event, 3),
                 "achieved": round(per_gpu_events * alg_per_event / 1e9, 1), "unit": "GB/s",
+                "peak": HBM_PEAK_GBS,
                 "frac": round(per_gpu_events * alg_per_event / 1e9 / HBM_PEAK_GBS, 4)}
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline_pattern(args, args.cpu_seconds) if pattern else \
-            cpu_baseline_filter(args, n, args.cpu_seconds)
 
     if rank == 0:
         out = {
@@ -358,9 +423,11 @@ def main():
                         "events_per_step_per_gpu": n, "parallelism": "replicas x%d" % world}),
             "matches_per_s": round(matches_total / dt_max, 1),
             "matches_per_event": round(m_per_event, 5),
-            "roofline": roofline,
             "pipeline_roofline": pipeline,
+            "roofline": roofline,
+            "roofline_kernels": per_kernel,
             "kernels": kern,
+            "parity": parity,
             "cpu_baseline": cpu,
             "speedup_vs_cpu_baseline": round(value / cpu["value"], 1) if cpu else None,
         }

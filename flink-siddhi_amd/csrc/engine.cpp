@@ -108,6 +108,7 @@ struct cep_app {
   hipStream_t side = nullptr;    // partition pass of the next chunk
   hipEvent_t in_ready = nullptr;
   hipEvent_t ext_ready = nullptr;   // cep_stream_wait: producer stream of device inputs
+  hipEvent_t out_ready = nullptr;   // cep_stream_signal: the engine's work so far
   bool enabled = true;
   std::string last_error;
   std::vector<std::string> dict;
@@ -130,7 +131,7 @@ struct cep_app {
     DevBuf out[kMaxCols], ots, ostream;   // sorted released rows (a device batch)
     DevBuf keys, idx_in, idx_out, temp, bound;
   } ro;
-  int64_t events_in = 0, matches_out = 0, batches = 0;
+  int64_t events_in = 0, matches_out = 0, batches = 0, late_events = 0;
   int64_t last_ts = INT64_MIN;
   int64_t launches[16] = {0};
   double kernel_ms[16] = {0};
@@ -243,7 +244,8 @@ int create_runtime(cep_app* a) {
   if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&a->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&a->in_ready, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&a->ext_ready, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&a->ext_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&a->out_ready, hipEventDisableTiming) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
@@ -914,6 +916,7 @@ void cep_destroy(cep_app* a) {
     }
   if (a->in_ready) hipEventDestroy(a->in_ready);
   if (a->ext_ready) hipEventDestroy(a->ext_ready);
+  if (a->out_ready) hipEventDestroy(a->out_ready);
   if (a->side) hipStreamDestroy(a->side);
   if (a->stream) hipStreamDestroy(a->stream);
   delete a;
@@ -1072,17 +1075,23 @@ int cep_watermark(cep_app* a, int64_t mark) {
                    (int32_t*)r.idx_out.p, n, a->stream))
     return fail(a, CEP_E_DEVICE, "reorder sort failed");
   launch_upper_bound((const int64_t*)r.keys.p, n, mark, (int64_t*)r.bound.p, a->stream);
-  int64_t hb[3] = {0, 0, 0};
+  // rows older than one already released (late events) sort first: count them
+  const bool any_released = r.released_max != INT64_MIN;
+  if (any_released)
+    launch_upper_bound((const int64_t*)r.keys.p, n, r.released_max - 1, (int64_t*)r.bound.p + 3, a->stream);
+  int64_t hb[6] = {0, 0, 0, 0, 0, 0};
   if (hipMemcpyAsync(hb, r.bound.p, sizeof(hb), hipMemcpyDeviceToHost, a->stream) != hipSuccess ||
       hipStreamSynchronize(a->stream) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "device failure during processing");
   const int64_t rel = hb[0];
   if (rel == 0) return CEP_OK;
-  // a row at or before an earlier watermark arrived late: the reference hands
-  // it to Siddhi out of order; `within` needs event-time order, so refuse
-  if (hb[1] < r.released_max)
-    return fail(a, CEP_E_ARG, "late event: ts " + std::to_string(hb[1]) + " is before already released ts " +
-                                  std::to_string(r.released_max));
+  // A row older than an earlier watermark's release arrived late.  The
+  // reference hands it to Siddhi out of order (AbstractSiddhiOperator.java:
+  // 238-245); `within` needs event-time order, so late rows are dropped (as
+  // Flink drops late elements) and counted in cep_stats.late_events; the
+  // on-time rows are released and the buffer stays consistent.
+  const int64_t late = any_released ? std::min(hb[3], rel) : 0;
+  a->late_events += late;
   const int32_t* perm = (const int32_t*)r.idx_out.p;
   bool ok = true;
   for (int c = 0; c < nc && ok; ++c) {
@@ -1109,13 +1118,13 @@ int cep_watermark(cep_app* a, int64_t mark) {
   r.n = keep;
   const int input = r.input;
   if (keep == 0) r.input = -1;
-  // the released prefix is a device batch in event-time order
+  // the released prefix minus the late rows is a device batch in event-time order
   const void* cols[kMaxCols];
-  for (int c = 0; c < nc; ++c) cols[c] = r.out[c].p;
+  for (int c = 0; c < nc; ++c) cols[c] = (const char*)r.out[c].p + late * type_width(sd.attrs[c].type);
   cep_batch bb{};
-  bb.n = rel;
-  bb.ts = (const int64_t*)r.ots.p;
-  bb.stream = r.has_stream ? (const uint8_t*)r.ostream.p : nullptr;
+  bb.n = rel - late;
+  bb.ts = (const int64_t*)r.ots.p + late;
+  bb.stream = r.has_stream ? (const uint8_t*)r.ostream.p + late : nullptr;
   bb.input = input;
   bb.ncols = nc;
   bb.cols = cols;
@@ -1123,7 +1132,7 @@ int cep_watermark(cep_app* a, int64_t mark) {
   a->last_ts = r.released_max;   // the kernel's order check spans the watermark
   const int64_t rmax = hb[2];
   int rc = cep_send_batch(a, &bb);
-  if (rc == CEP_OK) r.released_max = rmax;
+  if (rc == CEP_OK) r.released_max = std::max(r.released_max, rmax);
   // the sorted batch buffers are reused by the next watermark: finish first
   hipStreamSynchronize(a->stream);
   return rc;
@@ -1135,10 +1144,18 @@ int cep_flush(cep_app* a) {
     return fail(a, CEP_E_DEVICE, "device failure during processing");
   harvest_timers(a);
   int rc = check_device_error(a);
+  // an output cursor past its capacity is a hard failure before any count
+  // is used (the rows beyond cap were never written)
   for (auto& o : a->outs) {
     unsigned long long cnt = 0;
     hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
-    if (cnt > (unsigned long long)o.cap) cnt = o.cap;
+    if (cnt > (unsigned long long)o.cap && rc == CEP_OK)
+      rc = fail(a, CEP_E_DEVICE, "output capacity exceeded on " + o.id + ": " + std::to_string(cnt) +
+                                     " rows > " + std::to_string(o.cap));
+  }
+  for (auto& o : a->outs) {
+    unsigned long long cnt = 0;
+    if (rc == CEP_OK) hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
     a->matches_out += (int64_t)cnt;
     if (o.fn && cnt > 0 && rc == CEP_OK) {
       const size_t n = cnt;
@@ -1203,11 +1220,13 @@ int cep_output_device(cep_app* a, const char* out_id, cep_rows* rows) {
   OutStream& o = a->outs[i];
   unsigned long long cnt = 0;
   hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
+  if (cnt > (unsigned long long)o.cap)
+    return fail(a, CEP_E_DEVICE, "output capacity exceeded on " + o.id);
   static thread_local std::vector<const void*> ptrs;
   ptrs.assign(o.cols.size(), nullptr);
   for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.cols[c].p;
   rows->stream_id = o.id.c_str();
-  rows->n = (int64_t)std::min<unsigned long long>(cnt, (unsigned long long)o.cap);
+  rows->n = (int64_t)cnt;
   rows->ncols = (int32_t)o.cols.size();
   rows->ts = (const int64_t*)o.ts.p;
   rows->seq = (const int64_t*)o.seq.p;
@@ -1229,6 +1248,14 @@ int cep_stream_wait(cep_app* a, void* hip_stream) {
   if (hipEventRecord(a->ext_ready, (hipStream_t)hip_stream) != hipSuccess ||
       hipStreamWaitEvent(a->stream, a->ext_ready, 0) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "cep_stream_wait: invalid stream");
+  return CEP_OK;
+}
+
+int cep_stream_signal(cep_app* a, void* hip_stream) {
+  if (!a) return CEP_E_ARG;
+  if (hipEventRecord(a->out_ready, a->stream) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)hip_stream, a->out_ready, 0) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "cep_stream_signal: invalid stream");
   return CEP_OK;
 }
 
@@ -1261,6 +1288,7 @@ int cep_stats(cep_app* a, cep_stats_t* s) {
   s->events_in = a->events_in;
   s->matches_out = a->matches_out;
   s->batches = a->batches;
+  s->late_events = a->late_events;
   for (int i = 0; i < 16; ++i) {
     s->kernel_launches[i] = a->launches[i];
     s->kernel_ms[i] = a->kernel_ms[i];
@@ -1273,10 +1301,15 @@ const char* cep_last_error(cep_app* a) { return a ? a->last_error.c_str() : "nul
 
 void cep_free(void* p) { std::free(p); }
 
-// Snapshot format (little endian):
-//   "CEPS" u32 version=2, u64 plan_hash, i64 events_in, u32 n_patterns,
+// Snapshot format (little endian), version 3:
+//   "CEPS" u32 version, u64 plan_hash, i64 events_in, u32 n_patterns,
 //   per pattern: i64 key_capacity, u32 S, u32 slot_words, u32 n_live,
 //                n_live x { u32 key, u64 header, (header & 0xff) * slot_words u64 }
+//   (version >= 3) the event-time reorder buffer ("queuedRecordsState",
+//   AbstractSiddhiOperator.java:98): i32 input (-1: empty), u8 has_stream,
+//   i64 n, i64 released_max, then n rows: every column of the input's
+//   definition (type width each), n x i64 ts, n x u8 stream if has_stream.
+// Version 2 (no reorder section) is still restored.
 static uint64_t plan_hash(const CompiledApp& app) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](const void* p, size_t n) {
@@ -1364,7 +1397,7 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   if (!a || (!buf && len)) return CEP_E_ARG;
   size_t off = 0;
   auto get = [&](void* p, size_t n) -> bool {
-    if (off + n > len) return false;
+    if (n > len - off) return false;
     std::memcpy(p, buf + off, n);
     off += n;
     return true;
@@ -1379,8 +1412,15 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     return fail(a, CEP_E_STATE, "not a libcep snapshot");
   if (h != plan_hash(a->app) || np != a->pats.size())
     return fail(a, CEP_E_STATE, "snapshot was taken with a different plan");
-  hipStreamSynchronize(a->stream);
-  for (auto& rt : a->pats) {
+  // Phase 1: parse and validate everything into host buffers; nothing on the
+  // device changes until the whole snapshot is known to be good.
+  struct PatState {
+    std::vector<uint32_t> hdr;
+    std::vector<uint64_t> slots;
+  };
+  std::vector<PatState> ps(a->pats.size());
+  for (size_t pi = 0; pi < a->pats.size(); ++pi) {
+    const PatternRT& rt = a->pats[pi];
     int64_t kc;
     uint32_t S, sw, live;
     if (!get(&kc, 8) || !get(&S, 4) || !get(&sw, 4) || !get(&live, 4))
@@ -1388,56 +1428,75 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     if (kc != rt.pa.key_capacity || S != (uint32_t)rt.pa.pending_slots ||
         sw != (uint32_t)rt.pa.slot_words)
       return fail(a, CEP_E_STATE, "snapshot geometry differs from this runtime");
+    if ((uint64_t)live > (uint64_t)kc) return fail(a, CEP_E_STATE, "corrupt snapshot (live keys)");
     const int64_t ks = rt.kstride;
     const int lg = rt.pa.buckets_log2;
     const int64_t kpb = ks >> lg;
-    std::vector<uint32_t> hdr(ks, 0);
-    std::vector<uint64_t> slots((size_t)ks * S * sw, 0);
+    ps[pi].hdr.assign(ks, 0);
+    ps[pi].slots.assign((size_t)ks * S * sw, 0);
     for (uint32_t i = 0; i < live; ++i) {
       uint32_t key;
       uint64_t h64;
       if (!get(&key, 4) || !get(&h64, 8) || key >= kc || (h64 & 0xff) > S)
         return fail(a, CEP_E_STATE, "corrupt snapshot");
       const int64_t idx = (int64_t)(key & ((1u << lg) - 1)) * kpb + (key >> lg);
-      hdr[idx] = (uint32_t)h64;
+      ps[pi].hdr[idx] = (uint32_t)h64;
       for (uint32_t j = 0; j < (h64 & 0xff); ++j)
         for (uint32_t w = 0; w < sw; ++w)
-          if (!get(&slots[((size_t)j * sw + w) * ks + idx], 8))
+          if (!get(&ps[pi].slots[((size_t)j * sw + w) * ks + idx], 8))
             return fail(a, CEP_E_STATE, "truncated snapshot");
     }
-    hipMemcpy(rt.khdr.p, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice);
-    hipMemcpy(rt.kslot.p, slots.data(), slots.size() * 8, hipMemcpyHostToDevice);
   }
-  auto& r = a->ro;
-  r.n = 0;
-  r.input = -1;
-  r.released_max = INT64_MIN;
+  int32_t in = -1;
+  uint8_t hs = 0;
+  int64_t n = 0, rmax = INT64_MIN;
+  size_t rows_off = 0;
   if (ver >= 3) {
-    int32_t in;
-    uint8_t hs;
-    int64_t n, rmax;
-    if (!get(&in, 4) || !get(&hs, 1) || !get(&n, 8) || !get(&rmax, 8) || n < 0 ||
+    if (!get(&in, 4) || !get(&hs, 1) || !get(&n, 8) || !get(&rmax, 8) || n < 0 || n > (int64_t)INT32_MAX ||
         (n > 0 && (in < 0 || in >= (int)a->app.inputs.size())))
       return fail(a, CEP_E_STATE, "corrupt snapshot (reorder buffer)");
-    r.released_max = rmax;
     if (n > 0) {
-      const StreamSchema& sd = a->app.inputs[in];
-      auto push = [&](DevBuf* b, size_t bytes) -> bool {
-        if (off + bytes > len || !dev_ensure(b, bytes, a->stream, false)) return false;
-        hipMemcpy(b->p, buf + off, bytes, hipMemcpyHostToDevice);
-        off += bytes;
-        return true;
-      };
-      bool ok = true;
-      for (size_t c = 0; c < sd.attrs.size() && ok; ++c)
-        ok = push(&r.col[c], (size_t)n * type_width(sd.attrs[c].type));
-      ok = ok && push(&r.ts, (size_t)n * 8);
-      if (hs) ok = ok && push(&r.stream, (size_t)n);
-      if (!ok) return fail(a, CEP_E_STATE, "truncated snapshot (reorder buffer)");
-      r.input = in;
-      r.has_stream = hs != 0;
-      r.n = n;
+      size_t row_bytes = 8 + (hs ? 1 : 0);
+      for (auto& at : a->app.inputs[in].attrs) row_bytes += (size_t)type_width(at.type);
+      if ((uint64_t)n > (len - off) / row_bytes)
+        return fail(a, CEP_E_STATE, "truncated snapshot (reorder buffer)");
+      rows_off = off;
     }
+  }
+  // Phase 2: commit (device allocations first, so a failure leaves the
+  // runtime as it was)
+  auto& r = a->ro;
+  if (n > 0) {
+    const StreamSchema& sd = a->app.inputs[in];
+    bool ok = true;
+    for (size_t c = 0; c < sd.attrs.size() && ok; ++c)
+      ok = dev_ensure(&r.col[c], (size_t)n * type_width(sd.attrs[c].type), a->stream, false);
+    ok = ok && dev_ensure(&r.ts, (size_t)n * 8, a->stream, false);
+    if (hs) ok = ok && dev_ensure(&r.stream, (size_t)n, a->stream, false);
+    if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (reorder buffer)");
+  }
+  hipStreamSynchronize(a->stream);
+  for (size_t pi = 0; pi < a->pats.size(); ++pi) {
+    hipMemcpy(a->pats[pi].khdr.p, ps[pi].hdr.data(), ps[pi].hdr.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(a->pats[pi].kslot.p, ps[pi].slots.data(), ps[pi].slots.size() * 8, hipMemcpyHostToDevice);
+  }
+  r.n = 0;
+  r.input = -1;
+  r.released_max = rmax;
+  if (n > 0) {
+    const StreamSchema& sd = a->app.inputs[in];
+    size_t o = rows_off;
+    for (size_t c = 0; c < sd.attrs.size(); ++c) {
+      const size_t bytes = (size_t)n * type_width(sd.attrs[c].type);
+      hipMemcpy(r.col[c].p, buf + o, bytes, hipMemcpyHostToDevice);
+      o += bytes;
+    }
+    hipMemcpy(r.ts.p, buf + o, (size_t)n * 8, hipMemcpyHostToDevice);
+    o += (size_t)n * 8;
+    if (hs) hipMemcpy(r.stream.p, buf + o, (size_t)n, hipMemcpyHostToDevice);
+    r.input = in;
+    r.has_stream = hs != 0;
+    r.n = n;
   }
   a->events_in = ev;
   return CEP_OK;
@@ -1460,6 +1519,10 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
     return fail(a, CEP_E_UNSUPPORTED, "key shuffle needs a partitioned pattern");
   for (int d = 0; d < world; ++d) counts_host[d] = 0;
   if (b->n == 0) return CEP_OK;
+  // the gather writes rec_out as soon as it runs: at most n records are
+  // routed, so a buffer of n records can never overrun (checked up front)
+  if (!rec_out || rec_cap < b->n)
+    return fail(a, CEP_E_ARG, "rec_out must hold at least n records (" + std::to_string(b->n) + ")");
   RowsArgs rows{};
   int rc = batch_rows(a, b, &rows);
   if (rc) return rc;
@@ -1505,7 +1568,6 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
                    (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
     }
   }
-  // counts first: the gather must not overrun rec_out
   std::vector<unsigned long long> dc(world);
   hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, a->stream);
   if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "route failed");
@@ -1514,7 +1576,7 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
     counts_host[d] = (int64_t)dc[d];
     total += (int64_t)dc[d];
   }
-  if (total > rec_cap) return fail(a, CEP_E_CAPACITY, "rec_out holds fewer records than routed");
+  if (total > b->n) return fail(a, CEP_E_DEVICE, "route produced more records than rows");
   rc = check_device_error(a);
   if (rc) return rc;
   a->batches++;

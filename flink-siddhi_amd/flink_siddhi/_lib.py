@@ -114,7 +114,8 @@ class cep_rows(C.Structure):
 class cep_stats_t(C.Structure):
     _fields_ = [("events_in", C.c_int64), ("matches_out", C.c_int64),
                 ("batches", C.c_int64), ("kernel_launches", C.c_int64 * 16),
-                ("kernel_ms", C.c_double * 16), ("kernel_timed", C.c_int64 * 16)]
+                ("kernel_ms", C.c_double * 16), ("kernel_timed", C.c_int64 * 16),
+                ("late_events", C.c_int64)]
 
 
 EMIT_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(cep_rows))
@@ -146,6 +147,7 @@ SIGNATURES = {
     "cep_free": (None, [C.c_void_p]),
     "cep_set_enabled": (C.c_int, [C.c_void_p, C.c_int]),
     "cep_stream_wait": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "cep_stream_signal": (C.c_int, [C.c_void_p, C.c_void_p]),
     "cep_dict_intern": (C.c_int32, [C.c_void_p, C.c_char_p]),
     "cep_dict_lookup": (C.c_char_p, [C.c_void_p, C.c_int32]),
     "cep_stats": (C.c_int, [C.c_void_p, C.POINTER(cep_stats_t)]),

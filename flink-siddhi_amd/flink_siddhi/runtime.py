@@ -178,8 +178,8 @@ class SiddhiAppRuntime:
     def process_watermark(self, mark: int):
         """processWatermark (AbstractSiddhiOperator.java:238-247): buffered rows
         with ts <= mark reach the engine in (ts, arrival) order; later rows
-        stay buffered.  A row older than one already released raises
-        ValueError (late event)."""
+        stay buffered.  A row older than one already released (a late event)
+        is dropped and counted in stats().late_events."""
         self._check(self._lib.cep_watermark(self._h, int(mark)))
 
     def buffered(self) -> int:
@@ -208,6 +208,8 @@ class SiddhiAppRuntime:
         if on_device:
             self._wait_producer(ts)
         self._check(fn(self._h, C.byref(b)))
+        if on_device:
+            self._signal_consumer(ts)
 
     def _wait_producer(self, t):
         """Order the engine's stream after torch's current stream (device
@@ -215,6 +217,15 @@ class SiddhiAppRuntime:
         import torch
         s = torch.cuda.current_stream(t.device).cuda_stream
         self._check(self._lib.cep_stream_wait(self._h, C.c_void_p(s)))
+
+    def _signal_consumer(self, t):
+        """Order torch's current stream after the engine's queued work: the
+        caching allocator may hand a freed input tensor's memory to a later
+        kernel on that stream, which must not run while the engine still reads
+        it (cep.h, Ownership)."""
+        import torch
+        s = torch.cuda.current_stream(t.device).cuda_stream
+        self._check(self._lib.cep_stream_signal(self._h, C.c_void_p(s)))
 
     def flush(self):
         self._check(self._lib.cep_flush(self._h))
@@ -257,6 +268,7 @@ class SiddhiAppRuntime:
         self._wait_producer(ts)
         self._check(self._lib.cep_route_batch(self._h, C.byref(b), world, seq0,
                                               C.c_void_p(out.data_ptr()), out.shape[0], counts))
+        self._signal_consumer(ts)
         return out, [int(c) for c in counts]
 
     def send_records(self, recs, n: int, events_represented: int = 0):
@@ -265,11 +277,33 @@ class SiddhiAppRuntime:
         if n and getattr(recs, "is_cuda", False):
             self._wait_producer(recs)
         self._check(self._lib.cep_send_records(self._h, p, n, events_represented))
+        if n and getattr(recs, "is_cuda", False):
+            self._signal_consumer(recs)
 
     def output_device(self, out_id: str):
         r = L.cep_rows()
         self._check(self._lib.cep_output_device(self._h, out_id.encode(), C.byref(r)))
         return r
+
+    def output_tensors(self, out_id: str, copy: bool = True):
+        """Device-resident consumer: the unflushed rows of out_id as torch
+        CUDA tensors (ts, seq, [cols]) in device emission order (per-key
+        order with ordered_output=0).  copy=False aliases engine memory that
+        the next send / flush / reset_output invalidates."""
+        import torch
+        r = self.output_device(out_id)
+        n = int(r.n)
+        types = [t for _, t in self.stream_definition(out_id)]
+        dev = torch.device("cuda", int(self.options.device))
+
+        def wrap(ptr, dtype: str):
+            t = torch.as_tensor(_DevArray(ptr, n, dtype), device=dev)
+            return t.clone() if copy else t
+
+        ts = wrap(C.cast(r.ts, C.c_void_p).value, "<i8")
+        seq = wrap(C.cast(r.seq, C.c_void_p).value, "<i8")
+        cols = [wrap(r.cols[c], np.dtype(L.NUMPY_DTYPES[t]).str) for c, t in enumerate(types)]
+        return ts, seq, cols
 
     def reset_output(self):
         self._check(self._lib.cep_reset_output(self._h))
@@ -295,6 +329,16 @@ class SiddhiAppRuntime:
         s = L.cep_stats_t()
         self._check(self._lib.cep_stats(self._h, C.byref(s)))
         return s
+
+
+class _DevArray:
+    """A raw device buffer exposed through __cuda_array_interface__ (torch on
+    ROCm reads the same protocol) so torch can view engine output memory."""
+
+    def __init__(self, ptr, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
+                                         "data": (int(ptr or 0), False), "version": 3,
+                                         "strides": None}
 
 
 def _is_device(x) -> bool:

@@ -54,6 +54,48 @@ def generate(first: int, n: int, keys: int, rate: int = 400, seed: int = SEED,
     return {"k": key, "stream": stream, "id": idv, "price": price, "ts": ts}
 
 
+def _lsr(x, s: int):
+    """Logical right shift of int64 tensors (torch's >> is arithmetic)."""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def _smix_t(z):
+    z = z + (GOLDEN - (1 << 64))
+    z = (z ^ _lsr(z, 30)) * (0xBF58476D1CE4E5B9 - (1 << 64))
+    z = (z ^ _lsr(z, 27)) * (0x94D049BB133111EB - (1 << 64))
+    return z ^ _lsr(z, 31)
+
+
+def rows_digest(k, p1, p2, t, seq) -> int:
+    """Order-sensitive digest of config-3 output rows (torch tensors on any
+    device, rows in emission order): sum over rows of
+    oracle_row_digest(k, rank of the row among its key's rows, p1, p2, t,
+    seq) mod 2^64 — the same function as oracle/cep_oracle.c, so a bench or
+    test can compare the engine's device output with the oracle without
+    moving rows to the host.  Independent of how keys interleave, sensitive
+    to the order inside each key."""
+    import torch
+    n = int(k.shape[0])
+    if n == 0:
+        return 0
+    k64 = k.to(torch.int64)
+    order = torch.argsort(k64, stable=True)
+    ks = k64[order]
+    idx = torch.arange(n, device=k.device, dtype=torch.int64)
+    start = torch.zeros(n, dtype=torch.bool, device=k.device)
+    start[0] = True
+    start[1:] = ks[1:] != ks[:-1]
+    first = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), 0).values
+    rank = torch.empty_like(idx)
+    rank[order] = idx - first
+    x = _smix_t((k64 & 0xFFFFFFFF) | (rank << 32))
+    x = _smix_t(x ^ p1.contiguous().view(torch.int64))
+    x = _smix_t(x ^ p2.contiguous().view(torch.int64))
+    x = _smix_t(x ^ t.to(torch.int64))
+    x = _smix_t(x ^ seq.to(torch.int64))
+    return int(x.sum().item()) & ((1 << 64) - 1)
+
+
 def generate_device(first: int, n: int, keys: int, rate: int = 400, seed: int = SEED,
                     t0: int = T0, single_stream: bool = False, device="cuda"):
     """Same stream, generated on the GPU into torch tensors (bench inputs)."""

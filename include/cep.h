@@ -14,10 +14,15 @@
  * the analogue of StreamCallback.receive(Event[]) running synchronously in
  * InputHandler.send (operator/StreamOutputHandler.java:63).
  *
- * Ownership: input buffers stay owned by the caller and are consumed before
- * cep_send_batch() returns.  Output rows handed to the callback are owned by
- * the engine and valid only during the callback.  Snapshot buffers are
- * engine-allocated and released with cep_free().
+ * Ownership: input buffers stay owned by the caller.  Host batches are
+ * consumed before cep_send_batch() / cep_buffer_batch() return.  Device
+ * batches (on_device = 1) are read asynchronously on the engine's HIP
+ * stream: they must stay allocated and unchanged until that work is done —
+ * after cep_flush(), or, for a caller whose allocator reuses memory in
+ * stream order, after cep_stream_signal() has made the caller's stream wait
+ * for the engine.  Output rows handed to the callback are owned by the engine
+ * and valid only during the callback.  Snapshot buffers are engine-allocated
+ * and released with cep_free().
  */
 #ifndef CEP_H_
 #define CEP_H_
@@ -127,6 +132,7 @@ typedef struct {
   int64_t kernel_launches[16];
   double kernel_ms[16];       /* with cep_options.profile: summed HIP-event time */
   int64_t kernel_timed[16];   /* launches kernel_ms covers (profile = k: every k-th) */
+  int64_t late_events;        /* rows dropped by cep_watermark as late (ts before an earlier release) */
 } cep_stats_t;
 
 /* Kernel kinds indexing cep_stats_t arrays. */
@@ -182,7 +188,9 @@ int cep_buffer_batch(cep_app* app, const cep_batch* batch);
  * rows with ts <= mark go to the engine in (ts, arrival) order (one stable
  * device sort; the reference PQ orders by ts only, StreamRecordComparator.java:
  * 32-40); later rows stay buffered.  A row older than one already released
- * (a late event) is refused with CEP_E_ARG: `within` needs event-time order. */
+ * (a late event) is dropped and counted in cep_stats_t.late_events — `within`
+ * needs event-time order; the reference would hand it to Siddhi out of order
+ * — and the on-time rows of the same watermark are released as usual. */
 int cep_watermark(cep_app* app, int64_t mark);
 
 /* Rows still buffered (the PriorityQueue's size). */
@@ -216,6 +224,14 @@ int cep_set_enabled(cep_app* app, int enabled);
  * sync).  Call before cep_send_batch / cep_route_batch / cep_send_records
  * with device pointers whose producer is still in flight. */
 int cep_stream_wait(cep_app* app, void* hip_stream);
+
+/* The reverse edge: everything queued on hip_stream after this call waits for
+ * the engine's work queued so far (event + stream wait, no host sync).  A
+ * framework that frees or reuses device input buffers in stream order (the
+ * torch caching allocator) calls it after cep_send_batch / cep_route_batch /
+ * cep_send_records so a recycled buffer is never overwritten while the
+ * engine still reads it. */
+int cep_stream_signal(cep_app* app, void* hip_stream);
 
 /* String dictionary (STRING columns carry int32 ids). */
 int32_t cep_dict_intern(cep_app* app, const char* s);

@@ -92,19 +92,41 @@ def test_watermark_releases_only_rows_at_or_before_it():
     assert_same_rows(got, want, "watermark split")
 
 
-def test_late_event_is_refused():
-    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
-    ts = np.arange(1000, 1100, dtype=np.int64)
-    z = np.zeros(100, dtype=np.int32)
-    p = np.full(100, 0.75)
-    st = np.zeros(100, dtype=np.uint8)
-    rt.process_elements("A", ts, [z, ts, z, p], streams=st)
+def test_late_event_is_dropped():
+    """A row older than an earlier watermark's release is dropped and counted
+    (ADVICE r1: it used to stay buffered and wedge every later watermark);
+    the on-time rows of the same watermark still go through, the buffer
+    drains, and later watermarks keep working."""
+    plan = workload.PATTERN_PLAN.replace("within 10 sec", "within 1 sec")
+    rt = fs.SiddhiAppRuntime(plan)
+    rt.add_callback("O")
+    n = 100
+    ts = np.arange(1000, 1000 + n, dtype=np.int64)
+    z = np.zeros(n, dtype=np.int32)
+    idv = np.where(np.arange(n) % 3 == 2, 7, 1).astype(np.int32)   # every 3rd row: a g-passing B
+    p = np.full(n, 0.75)
+    st = (np.arange(n) % 3 == 2).astype(np.uint8)
+    rt.process_elements("A", ts, [z, ts, idv, p], streams=st)
     rt.process_watermark(1050)
     late = np.array([1020], dtype=np.int64)
     rt.process_elements("A", late, [z[:1], late, z[:1], p[:1]], streams=st[:1])
-    with pytest.raises(ValueError):
-        rt.process_watermark(2000)
+    more = np.arange(1100, 1110, dtype=np.int64)
+    rt.process_elements("A", more, [z[:10], more, idv[:10], p[:10]], streams=st[:10])
+    rt.process_watermark(1105)     # releases 1051..1105, drops the late 1020
+    assert rt.stats().late_events == 1
+    assert rt.buffered() == 4
+    rt.process_watermark(2000)
+    assert rt.buffered() == 0
+    rt.flush()
+    got = engine_rows(rt.collect("O"))
     rt.shutdown()
+    allts = np.concatenate([ts, more])
+    cols = [np.concatenate([z, z[:10]]), allts, np.concatenate([idv, idv[:10]]), np.concatenate([p, p[:10]])]
+    stv = np.concatenate([st, st[:10]])
+    ev = [("AB"[stv[i]], int(allts[i]), tuple(c[i].item() for c in cols)) for i in range(len(allts))]
+    want = oracle_run(plan, ev).get("O", [])
+    assert len(want) > 0
+    assert_same_rows(got, want, "late row dropped")
 
 
 def test_reordered_filter_matches_oracle():
@@ -162,3 +184,65 @@ def test_snapshot_keeps_rows_waiting_for_a_watermark():
     second = engine_rows(rt2.collect("O"))
     rt2.shutdown()
     assert_same_rows(first + second, want, "reorder snapshot/restore")
+
+
+def test_restore_rejects_truncated_snapshot_and_keeps_state():
+    """A v3 snapshot cut inside the reorder-buffer rows is refused before
+    anything on the device changes (restore used to commit while
+    parsing); the untouched runtime keeps working."""
+    w = disordered(20000, 1024, 2, jitter=600, seed=9)
+    half = 12000
+    suffix_min = np.minimum.accumulate(w["ts"][::-1])[::-1]
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt.process_elements("A", w["ts"][:half], [w["k"][:half], w["ts"][:half], w["id"][:half], w["price"][:half]],
+                        streams=w["stream"][:half])
+    rt.process_watermark(int(suffix_min[half]) - 1)
+    held = rt.buffered()
+    assert held > 0
+    rt.flush()
+    snap = rt.snapshot()
+    rt.shutdown()
+    rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    for cut in (len(snap) - 1, len(snap) - held * 5, 30):
+        with pytest.raises(fs.CepStateError):
+            rt2.restore(snap[:cut])
+        assert rt2.buffered() == 0
+    # a lying row count (n huge, bytes short) is refused too
+    import struct
+    body = bytearray(snap)
+    tail = len(body) - held * (4 + 8 + 4 + 8 + 8 + 1)    # columns k ts id price + event ts + stream
+    n_off = tail - 8 - 8                                   # i64 n, i64 released_max precede the rows
+    assert struct.unpack_from("<q", body, n_off)[0] == held
+    struct.pack_into("<q", body, n_off, (1 << 31) - 1)
+    with pytest.raises(fs.CepStateError):
+        rt2.restore(bytes(body))
+    rt2.restore(snap)
+    assert rt2.buffered() == held
+    rt2.shutdown()
+
+
+def test_restore_version2_snapshot():
+    """Version-2 snapshots (per-key state only, no reorder section) still load."""
+    import struct
+    w = workload.generate(0, 30000, 2048, rate=1)
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(w)).get("O", [])
+    h = 17000
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt.add_callback("O")
+    rt.send("A", w["ts"][:h], [w["k"][:h], w["ts"][:h], w["id"][:h], w["price"][:h]], streams=w["stream"][:h])
+    rt.flush()
+    first = engine_rows(rt.collect("O"))
+    snap = bytearray(rt.snapshot())
+    rt.shutdown()
+    assert struct.unpack_from("<I", snap, 4)[0] == 3
+    # empty reorder section: i32 input, u8 has_stream, i64 n, i64 released_max
+    v2 = snap[:-21]
+    struct.pack_into("<I", v2, 4, 2)
+    rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt2.add_callback("O")
+    rt2.restore(bytes(v2))
+    rt2.send("A", w["ts"][h:], [w["k"][h:], w["ts"][h:], w["id"][h:], w["price"][h:]], streams=w["stream"][h:])
+    rt2.flush()
+    second = engine_rows(rt2.collect("O"))
+    rt2.shutdown()
+    assert_same_rows(first + second, want, "v2 restore")

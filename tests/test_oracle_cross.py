@@ -43,3 +43,38 @@ def test_c_oracle_filter_matches_python():
           zip(w["id"].tolist(), w["price"].tolist(), w["ts"].tolist())]
     want = oracle_run(workload.FILTER_PLAN, ev)["O"]
     assert [s for _, s, _ in want] == sel.tolist()
+
+
+def test_c_generator_and_sharded_digest():
+    """oracle_generate == workload.generate; the key-sharded C oracle gives
+    the same matches and order-sensitive digest at every thread count; the
+    torch digest (bench.py's engine side) equals the C digest of the
+    single-thread oracle's pairs."""
+    import numpy as np
+    import torch
+    import cep_oracle as CO
+    from flink_siddhi import workload
+    w = workload.generate(1000, 150000, 4096, rate=3)
+    w2 = CO.generate(1000, 150000, 4096, rate=3, threads=5)
+    for c in w:
+        assert np.array_equal(w[c], w2[c]), c
+    f, g = CO.cond(("price", 0, ">", 0.5)), CO.cond(("id", 7, "==", 0))
+    res = {T: CO.pattern_mt(w, 4096, f, g, True, 100, threads=T, idx0=1000)[:2] for T in (1, 3, 8)}
+    assert len(set(res.values())) == 1, res
+    po = CO.PatternOracle(4096, f, g, True, 100)
+    po.idx = 1000
+    a, b, m = po.run(w)
+    assert (m, ) == (res[1][0], ) and m > 100
+    ai, bi = a - 1000, b - 1000
+    t = torch.from_numpy
+    d = workload.rows_digest(t(w["k"][ai]), t(w["price"][ai]), t(w["price"][bi]), t(w["ts"][bi]), t(b))
+    assert d == res[1][1]
+    # order sensitivity: swapping two rows of one key changes the digest
+    k = w["k"][ai]
+    dup = np.nonzero(np.bincount(k) >= 2)[0][0]
+    i, j = np.nonzero(k == dup)[0][:2]
+    perm = np.arange(len(ai))
+    perm[[i, j]] = perm[[j, i]]
+    d2 = workload.rows_digest(t(k[perm]), t(w["price"][ai][perm]), t(w["price"][bi][perm]),
+                              t(w["ts"][bi][perm]), t(b[perm]))
+    assert d2 != d
