@@ -338,16 +338,17 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   // order); each row's final rank is the number of rows of its segment with
   // a smaller row index: a scan of the segment's rows for short segments, a
   // row bitmap + popcount prefix for the few long ones (hot keys).
-  // (the final rank replaces the atomic rank in packed[e]'s low 13 bits)
+  // (the final rank replaces the atomic rank in packed[e]'s low 13 bits;
+  // only k_cfwalk2 needs it: a.stable, uniform)
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < E && a.stable; ++e) {
     if (packed[e] == 0xffffffffu) continue;
     const uint32_t b = (packed[e] >> 13) & 0xfffu, rank = packed[e] & 0x1fffu;
     srow[hist[b] + rank] = (uint16_t)(wave * 64 * E + 64 * e + lane);
   }
-  lds_barrier();
+  if (a.stable) lds_barrier();
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < E && a.stable; ++e) {
     if (packed[e] == 0xffffffffu) continue;
     const uint32_t b = (packed[e] >> 13) & 0xfffu;
     const uint32_t b0 = hist[b], b1 = hist[b + 1];
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
       packed[e] = (packed[e] & ~0x1fffu) | r;
     }
   }
-  const uint32_t nb = nbig;   // uniform
+  const uint32_t nb = a.stable ? nbig : 0u;   // uniform
   for (uint32_t g0 = 0; g0 < nb; g0 += kBigGroup) {
     for (int i = tid; i < kBigGroup * (kCfTile / 32); i += NT) bbits[i] = 0;
     lds_barrier();
@@ -1297,6 +1298,9 @@ namespace {
 template <int NW>
 constexpr int w2_window() { return NW > 1 ? 1536 : 2048; }
 
+#ifndef CF_W2_OCC
+#define CF_W2_OCC 4
+#endif
 constexpr uint32_t kW2None = 0x7fffu;   // no next B
 constexpr uint32_t kW2Match = 0x8000u;  // snb flag: this A matches its next B
 
@@ -1309,8 +1313,12 @@ struct W2Lds {
   uint16_t sidx[WIN];                    // wave regions: sorted position -> group region index
   uint16_t snb[WIN];                     // wave regions: next B sorted position | kW2Match
   uint32_t gcnt[8][8];                   // records per (wave, key group)
-  uint32_t kcur[8][64];                  // per wave and key: run length, then sort cursor
-  uint16_t kfb[kCfMaxKeys], klb[kCfMaxKeys];   // per key: first / last B of its run (sorted position)
+  union {                                // per wave: its sort is done before its 4b starts
+    uint32_t kcur[64];                   // per key of the wave: run length, then sort cursor
+    struct {
+      uint16_t kfb[64], klb[64];         // per key of the wave: first / last B of its run (sorted position)
+    };
+  } wk[8];
   uint32_t wtot[8];                      // output rows per wave
   uint32_t scratch[kCfWalkThreads / 64 + 1];
   unsigned long long base;
@@ -1333,7 +1341,19 @@ __device__ __forceinline__ uint64_t peers6(uint32_t k6, bool v) {
 }  // namespace
 
 template <int NW>
-__global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
+// Diagnostics (CEP_STAMPS=1): cycles per walk2 phase, summed over the
+// block's windows (thread 0's view; every phase ends at a barrier).
+#define W2_PH(i)                                                                           \
+  do {                                                                                     \
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096) {                               \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                    \
+      atomicAdd((unsigned long long*)&a.stamps[(int64_t)blockIdx.x * 16 + (i)],            \
+                (unsigned long long)(t_ - ph_t));                                          \
+      ph_t = t_;                                                                           \
+    }                                                                                      \
+  } while (0)
+
+__global__ __launch_bounds__(kCfWalkThreads, CF_W2_OCC) void k_cfwalk2(CfWalkArgs a) {
   constexpr int NT = kCfWalkThreads, RW = 1 + NW, WIN = w2_window<NW>();
   constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
   constexpr int PER = WIN / NT;           // window slots per thread
@@ -1352,6 +1372,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
   const int S = p.pending_slots;
   const int64_t W = p.within;
   const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
+  uint64_t ph_t = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
   // ---- key lane (tid < kpb): pending count + slots 0 / 1 in registers
   const bool klane = tid < kpb;
@@ -1434,23 +1455,17 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
   };
 
   // ---- the bucket's segment of every tile: exclusive prefix over tiles
-  uint32_t spre[TPT];
+  // (this thread's first tile; the others follow from the segment sizes)
+  uint32_t spre0;
   uint32_t nall;
   {
-    uint32_t sum = 0, cnt[TPT];
+    uint32_t sum = 0;
 #pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      cnt[i] = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
-      sum += cnt[i];
-    }
-    uint32_t off = bscan<NT>(sum, L.scratch, &nall);
-#pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      spre[i] = off;
-      off += cnt[i];
-    }
+    for (int i = 0; i < TPT; ++i)
+      sum += ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
+    spre0 = bscan<NT>(sum, L.scratch, &nall);
   }
-  CF_STAMP(1);
+  W2_PH(0);
 
   for (uint32_t wb = 0; wb < nall; wb += WIN) {
     const uint32_t nw = min((uint32_t)WIN, nall - wb);
@@ -1458,20 +1473,21 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
     // values of step 1 out of the window loop (that many live registers spill)
 #pragma unroll
     for (int i = 0; i < TPT / 2; ++i) asm volatile("" : "+v"(lop[i]), "+v"(ys[i]));
-#pragma unroll
-    for (int i = 0; i < TPT; ++i) asm volatile("" : "+v"(spre[i]));
+    asm volatile("" : "+v"(spre0));
     // ---- 1. window slot -> arena record index
+    uint32_t s0 = spre0;
 #pragma unroll
     for (int i = 0; i < TPT; ++i) {
       const uint32_t st = (lop[i >> 1] >> (16 * (i & 1))) & 0xffffu;
       const uint32_t c = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - st;
-      const uint32_t s0 = spre[i];
       const uint32_t lo = max(s0, wb), hi = min(s0 + c, wb + nw);
       const uint32_t g0 = (uint32_t)(tb + i) * (uint32_t)kCfTile + st;
       for (uint32_t g = lo; g < hi; ++g) L.wrec[g - wb] = g0 + (g - s0);
+      s0 += c;
     }
-    (&L.kcur[0][0])[tid] = 0;   // 8 x 64 = NT entries
+    L.wk[wave].kcur[lane] = 0;
     lds_barrier();
+    W2_PH(1);
 
     // ---- 2. gather (wave w: slots [w * 64 * PER, (w + 1) * 64 * PER), arrival
     // order (i, lane)); stable rank per key group inside the wave
@@ -1513,6 +1529,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
       if (lane < 8) L.gcnt[wave][lane] = mine;
     }
     lds_barrier();
+    W2_PH(2);
 
     // ---- 3. group regions: (group, wave)-major offsets from one wave scan
     uint32_t gs, gn;
@@ -1544,7 +1561,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
       }
     }
     lds_barrier();
-    CF_STAMP(2);
+    W2_PH(3);
 
     // ---- 4a. per wave: stable counting sort of the group region by key
     uint32_t kc, kst;
@@ -1554,9 +1571,9 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
         const bool v = pp < gn;
         const uint32_t k6 = v ? (L.gmeta[gs + pp] >> 14) & 63u : 0u;
         const uint64_t m = peers6(k6, v);
-        if (v && (m & lt) == 0) L.kcur[wave][k6] += (uint32_t)__popcll(m);
+        if (v && (m & lt) == 0) L.wk[wave].kcur[k6] += (uint32_t)__popcll(m);
       }
-      kc = L.kcur[wave][lane];
+      kc = L.wk[wave].kcur[lane];
       uint32_t inc = kc;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -1564,23 +1581,23 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
         if (lane >= o) inc += t;
       }
       kst = inc - kc;
-      L.kcur[wave][lane] = kst;
+      L.wk[wave].kcur[lane] = kst;
       for (uint32_t c0 = 0; c0 < gn; c0 += 64) {
         const uint32_t pp = c0 + lane;
         const bool v = pp < gn;
         const uint32_t k6 = v ? (L.gmeta[gs + pp] >> 14) & 63u : 0u;
         const uint64_t m = peers6(k6, v);
-        const uint32_t b = L.kcur[wave][k6];
-        if (v && (m & lt) == 0) L.kcur[wave][k6] = b + (uint32_t)__popcll(m);
+        const uint32_t b = L.wk[wave].kcur[k6];
+        if (v && (m & lt) == 0) L.wk[wave].kcur[k6] = b + (uint32_t)__popcll(m);
         if (v) L.sidx[gs + b + (uint32_t)__popcll(m & lt)] = (uint16_t)(gs + pp);
       }
     }
+    W2_PH(4);
     // ---- 4b. right-to-left: next B of every sorted position, record matches
     uint32_t amatch = 0;
     {
-      const int key0 = wave * 64;
-      L.kfb[key0 + lane] = (uint16_t)kW2None;
-      L.klb[key0 + lane] = (uint16_t)kW2None;
+      L.wk[wave].kfb[lane] = (uint16_t)kW2None;
+      L.wk[wave].klb[lane] = (uint16_t)kW2None;
       uint32_t cnb = kW2None, cts = 0;
       const int nch = (int)((gn + 63) >> 6);
       for (int ch = nch - 1; ch >= 0; --ch) {
@@ -1616,8 +1633,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
           match = W < 0 || (d < 0 ? -d : d) <= W;
         }
         if (v) L.snb[gs + sp] = (uint16_t)(nb | (match ? kW2Match : 0u));
-        if (sstart) L.kfb[key0 + k6] = (uint16_t)(isB ? sp : nb);
-        if (isB && nb == kW2None) L.klb[key0 + k6] = (uint16_t)sp;
+        if (sstart) L.wk[wave].kfb[k6] = (uint16_t)(isB ? sp : nb);
+        if (isB && nb == kW2None) L.wk[wave].klb[k6] = (uint16_t)sp;
         amatch += (uint32_t)__popcll(__ballot(match));
         // carry into the chunk on the left: the first B of the run that
         // continues across the chunk border, if any
@@ -1634,10 +1651,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
         }
       }
     }
+    W2_PH(5);
     // ---- key lanes: carried partials completed by the run's first B
     const int kl = wave * 64 + lane;           // key in bucket
     const bool hasrun = klane && kc > 0;
-    const uint32_t kfb = L.kfb[kl], klb = L.klb[kl];
+    const uint32_t kfb = L.wk[wave].kfb[lane], klb = L.wk[wave].klb[lane];
     int cfirst = n, cm = 0;
     int64_t fbts = 0;
     if (hasrun && kfb != kW2None && n > 0) {
@@ -1664,6 +1682,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
     }
     if (lane == 0) L.wtot[wave] = cmw + amatch;
     lds_barrier();
+    W2_PH(6);
     if (tid == 0) {
       uint32_t t = 0;
 #pragma unroll
@@ -1671,7 +1690,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
       L.base = t ? atomicAdd(a.out.count, (unsigned long long)t) : 0ull;
     }
     lds_barrier();
-    CF_STAMP(3);
+    W2_PH(7);
     unsigned long long woff = L.base;
     for (int w = 0; w < wave; ++w) woff += L.wtot[w];
 
@@ -1729,6 +1748,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
       hdr = (hdr & ~0xffu) | (uint32_t)nn;
     }
 
+    W2_PH(8);
     // ---- 5b. record matches in (key, arrival) order
     {
       const unsigned long long o0 = woff + cmw;
@@ -1755,8 +1775,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
         run += (uint32_t)__popcll(m);
       }
     }
-    CF_STAMP(4);
     lds_barrier();   // the window's LDS is rewritten by the next one
+    W2_PH(9);
   }
   // ---- the key's header and register-resident slots 0 / 1, once
   if (klane && dirty) {
@@ -1772,11 +1792,16 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk2(CfWalkArgs a) {
     }
     a.khdr[kidx] = hdr;
   }
+  W2_PH(10);
+}
+
+bool cf_walk2_selected() {   // read per launch: tests switch it inside one process
+  const char* e = std::getenv("CEP_WALK");
+  return e && std::atoi(e) == 2;
 }
 
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
-  static const bool v1 = std::getenv("CEP_WALK_V1") != nullptr;   // A/B against the first walk
-  if (v1) {
+  if (!cf_walk2_selected()) {
     switch (a.cf.nw) {
       case 0: hipLaunchKernelGGL(k_cfwalk<0>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
       case 1: hipLaunchKernelGGL(k_cfwalk<1>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;

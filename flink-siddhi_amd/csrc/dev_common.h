@@ -134,7 +134,9 @@ __device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const in
                                                     const ColSet& cols,
                                                     const uint64_t (&vals)[kPref][N]) {
   uint32_t acc = tl.any ? 0u : ((N >= 32) ? 0xffffffffu : ((1u << N) - 1u));
-  for (int i = 0; i < tl.n; ++i) {
+#pragma unroll
+  for (int i = 0; i < kMaxTerms; ++i) {   // fixed indices: term descriptors load once (SGPRs)
+    if (i >= tl.n) break;
     const Term& t = tl.t[i];
     uint64_t v[N];
     take_slot<N>(vals, slot[i], v);   // one uniform branch, not a masked OR over every slot

@@ -200,6 +200,7 @@ constexpr int kCfMaxKeys = 512;                        // keys per bucket
 constexpr int kCfMaxTiles = (32 << 20) / kCfTile;      // chunk <= 32 Mi rows
 constexpr int kCfMaxBuckets = 4096;
 constexpr int kCfMaxCaps = 2;                          // captured words per pending slot
+constexpr int kCfMaxOut = 8;                           // select items on the fast path
 
 struct CfPlan {
   int32_t nw;                      // physical carried words per record (0..2)
@@ -224,6 +225,7 @@ struct CfPartArgs {
   uint16_t* tile_off;          // out: [P+1][ntiles] exclusive bucket offsets, bucket-major
   int32_t ntiles;
   uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per tile 16 s_memtime stamps
+  int32_t stable;              // 1: bucket segments in arrival order (k_cfwalk2 needs it)
   unsigned int* err;
 };
 
@@ -256,6 +258,7 @@ struct CfRouteArgs {
 // --------------------------------------------------------------- launchers --
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
+bool cf_walk2_selected();   // CEP_WALK=2: k_cfwalk2 instead of k_cfwalk
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
