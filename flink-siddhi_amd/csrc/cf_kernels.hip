@@ -28,8 +28,6 @@
 // resolves ~2.7 k records per launch instead of ~0.7 k.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
 #include "dev_common.h"
 #include "kernels.h"
 #include "vm.h"
@@ -163,15 +161,8 @@ template <int NW, bool FR>   // FR: rows are received shuffle records
 __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
-  constexpr int kSmallSeg = 48;     // segments up to this long are ranked by a scan
-  constexpr int kBigGroup = 4;      // long segments ranked together (one bitmap each)
   __shared__ uint32_t scratch[NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) uint64_t stage[kStageRecs * RW];
-  __shared__ uint16_t srow[kCfTile];                     // tile row per (scrambled) segment slot
-  __shared__ uint8_t bigid[kCfMaxBuckets];               // long segment number per bucket
-  __shared__ uint32_t bbits[kBigGroup * (kCfTile / 32)]; // row bitmaps of kBigGroup long segments
-  __shared__ uint32_t bpre[kBigGroup * (kCfTile / 32)];  // their popcount prefixes
-  __shared__ uint32_t nbig;
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // P + 1 (dynamic)
   const int tid = threadIdx.x;
   const int64_t tile = xcd_tile(blockIdx.x, a.ntiles);
@@ -298,12 +289,10 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
     const uint32_t rank = atomicAdd(&hist[bucket], 1u);
     packed[e] = (role << 25) | (bucket << 13) | rank;
   }
-  if (tid == 0) nbig = 0;
   lds_barrier();
   CF_STAMP(2);
   {
-    // exclusive scan of the P bucket counts (P <= 4096: <= 8 per thread);
-    // segments longer than kSmallSeg are registered for bitmap ranking
+    // exclusive scan of the P bucket counts (P <= 4096: <= 8 per thread)
     constexpr int MAXPER = kCfMaxBuckets / NT;
     const int per = (P + NT - 1) / NT;
     uint32_t c[MAXPER];
@@ -313,10 +302,6 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
       const int idx = tid * per + i;
       c[i] = (i < per && idx < P) ? hist[idx] : 0u;
       sum += c[i];
-      if (c[i] > (uint32_t)kSmallSeg) {
-        const uint32_t g = atomicAdd(&nbig, 1u);   // <= kCfTile / (kSmallSeg + 1) < 256 segments
-        bigid[idx] = (uint8_t)g;
-      }
     }
     uint32_t total;
     uint32_t off = bscan<NT>(sum, scratch, &total);
@@ -333,78 +318,6 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   lds_barrier();
   CF_STAMP(3);
   const uint32_t total = hist[P];
-  // ---- stable order inside each bucket segment (arrival order: the walk
-  // relies on it).  The histogram ranks above come from LDS atomics (any
-  // order); each row's final rank is the number of rows of its segment with
-  // a smaller row index: a scan of the segment's rows for short segments, a
-  // row bitmap + popcount prefix for the few long ones (hot keys).
-  // (the final rank replaces the atomic rank in packed[e]'s low 13 bits;
-  // only k_cfwalk2 needs it: a.stable, uniform)
-#pragma unroll
-  for (int e = 0; e < E && a.stable; ++e) {
-    if (packed[e] == 0xffffffffu) continue;
-    const uint32_t b = (packed[e] >> 13) & 0xfffu, rank = packed[e] & 0x1fffu;
-    srow[hist[b] + rank] = (uint16_t)(wave * 64 * E + 64 * e + lane);
-  }
-  if (a.stable) lds_barrier();
-#pragma unroll
-  for (int e = 0; e < E && a.stable; ++e) {
-    if (packed[e] == 0xffffffffu) continue;
-    const uint32_t b = (packed[e] >> 13) & 0xfffu;
-    const uint32_t b0 = hist[b], b1 = hist[b + 1];
-    const uint32_t row = (uint32_t)(wave * 64 * E + 64 * e + lane);
-    if (b1 - b0 <= (uint32_t)kSmallSeg) {
-      uint32_t r = 0;
-      for (uint32_t j = b0; j < b1; ++j) r += (uint32_t)srow[j] < row ? 1u : 0u;
-      packed[e] = (packed[e] & ~0x1fffu) | r;
-    }
-  }
-  const uint32_t nb = a.stable ? nbig : 0u;   // uniform
-  for (uint32_t g0 = 0; g0 < nb; g0 += kBigGroup) {
-    for (int i = tid; i < kBigGroup * (kCfTile / 32); i += NT) bbits[i] = 0;
-    lds_barrier();
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      if (packed[e] == 0xffffffffu) continue;
-      const uint32_t b = (packed[e] >> 13) & 0xfffu;
-      if (hist[b + 1] - hist[b] <= (uint32_t)kSmallSeg) continue;
-      const uint32_t g = bigid[b];
-      const uint32_t row = (uint32_t)(wave * 64 * E + 64 * e + lane);
-      if (g >= g0 && g < g0 + kBigGroup) atomicOr(&bbits[(g - g0) * (kCfTile / 32) + (row >> 5)], 1u << (row & 31));
-    }
-    lds_barrier();
-    {
-      // popcount prefix over the kBigGroup bitmaps (kBigGroup * 256 words)
-      constexpr int WPT = kBigGroup * (kCfTile / 32) / NT;   // words per thread
-      uint32_t pc[WPT], s = 0;
-#pragma unroll
-      for (int i = 0; i < WPT; ++i) {
-        pc[i] = (uint32_t)__popc(bbits[tid * WPT + i]);
-        s += pc[i];
-      }
-      uint32_t tot;
-      uint32_t o = bscan<NT>(s, scratch, &tot);
-#pragma unroll
-      for (int i = 0; i < WPT; ++i) {
-        bpre[tid * WPT + i] = o;
-        o += pc[i];
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      if (packed[e] == 0xffffffffu) continue;
-      const uint32_t b = (packed[e] >> 13) & 0xfffu;
-      if (hist[b + 1] - hist[b] <= (uint32_t)kSmallSeg) continue;
-      const uint32_t g = bigid[b];
-      if (g < g0 || g >= g0 + kBigGroup) continue;
-      const uint32_t row = (uint32_t)(wave * 64 * E + 64 * e + lane);
-      const uint32_t wb = (g - g0) * (kCfTile / 32);
-      packed[e] = (packed[e] & ~0x1fffu) |
-                  (bpre[wb + (row >> 5)] - bpre[wb] + (uint32_t)__popc(bbits[wb + (row >> 5)] & ((1u << (row & 31)) - 1u)));
-    }
-    lds_barrier();
-  }
   const bool staged = total <= (uint32_t)kStageRecs;   // uniform
   uint64_t* trecs = a.recs + tile * (int64_t)kCfTile * RW;
 #pragma unroll
@@ -1272,547 +1185,11 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
   }
 }
 
-// ============================================================= k_cfwalk2 ==
-// Walk, version 2: the same closed form as k_cfwalk with a wave-parallel
-// structure.  One 512-lane workgroup per key bucket; wave w owns the bucket's
-// keys [64 w, 64 w + 64) and lane j of wave w holds key 64 w + j's pending
-// state in registers.  Per window of WIN records (consecutive in arrival
-// order: k_cfpart writes every bucket segment in arrival order, tiles are in
-// arrival order):
-//   1. window slot -> arena record (each thread fills the slots of its tiles)
-//   2. gather into registers; each wave ranks its records per key group with
-//      ballots (stable: slot order = arrival order)
-//   3. records -> their group's region in LDS (arrival order per group)
-//   4. per wave, no barriers: stable counting sort of its region by key
-//      (ballot peer groups, per-key cursors in LDS), so each key's records
-//      are one arrival-ordered run;
-//      right-to-left pass over the sorted runs: next B of every position from
-//      ballots (segmented by run starts, carried across 64-position chunks);
-//      A matches its next B if within W; first / last B of each run
-//   5. one output-cursor atomic per workgroup-window; per wave: carried
-//      partials completed by the run's first B, new pending lists (A's after
-//      the run's last B, pruned), record matches in (key, arrival) order.
-// Six workgroup barriers per window; the per-key work is wave-local.
-namespace {
-
-template <int NW>
-constexpr int w2_window() { return NW > 1 ? 1536 : 2048; }
-
-#ifndef CF_W2_OCC
-#define CF_W2_OCC 4
-#endif
-constexpr uint32_t kW2None = 0x7fffu;   // no next B
-constexpr uint32_t kW2Match = 0x8000u;  // snb flag: this A matches its next B
-
-template <int NW, int WIN = w2_window<NW>()>
-struct W2Lds {
-  uint32_t wrec[WIN];                    // window slot -> arena record; after the gather: chunk row (arrival)
-  uint32_t gmeta[WIN];                   // group regions: slot (12) | A (1) << 12 | B (1) << 13 | key & 63 << 14
-  uint32_t gts[WIN];                     // group regions: ts - chunk ts base
-  uint64_t gcap[NW > 0 ? NW : 1][WIN];   // group regions: carried words
-  uint16_t sidx[WIN];                    // wave regions: sorted position -> group region index
-  uint16_t snb[WIN];                     // wave regions: next B sorted position | kW2Match
-  uint32_t gcnt[8][8];                   // records per (wave, key group)
-  union {                                // per wave: its sort is done before its 4b starts
-    uint32_t kcur[64];                   // per key of the wave: run length, then sort cursor
-    struct {
-      uint16_t kfb[64], klb[64];         // per key of the wave: first / last B of its run (sorted position)
-    };
-  } wk[8];
-  uint32_t wtot[8];                      // output rows per wave
-  uint32_t scratch[kCfWalkThreads / 64 + 1];
-  unsigned long long base;
-};
-
-__device__ __forceinline__ uint64_t lanes_above(int lane) { return lane == 63 ? 0ull : (~0ull << (lane + 1)); }
-
-// Lanes whose 6-bit value equals mine (among lanes with v set).
-__device__ __forceinline__ uint64_t peers6(uint32_t k6, bool v) {
-  uint64_t m = __ballot(v);
-#pragma unroll
-  for (int b = 0; b < 6; ++b) {
-    const bool bit = (k6 >> b) & 1u;
-    const uint64_t x = __ballot(bit);
-    m &= bit ? x : ~x;
-  }
-  return m;
-}
-
-}  // namespace
-
-template <int NW>
-// Diagnostics (CEP_STAMPS=1): cycles per walk2 phase, summed over the
-// block's windows (thread 0's view; every phase ends at a barrier).
-#define W2_PH(i)                                                                           \
-  do {                                                                                     \
-    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096) {                               \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                    \
-      atomicAdd((unsigned long long*)&a.stamps[(int64_t)blockIdx.x * 16 + (i)],            \
-                (unsigned long long)(t_ - ph_t));                                          \
-      ph_t = t_;                                                                           \
-    }                                                                                      \
-  } while (0)
-
-__global__ __launch_bounds__(kCfWalkThreads, CF_W2_OCC) void k_cfwalk2(CfWalkArgs a) {
-  constexpr int NT = kCfWalkThreads, RW = 1 + NW, WIN = w2_window<NW>();
-  constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
-  constexpr int PER = WIN / NT;           // window slots per thread
-  static_assert(PER * NT == WIN, "window = whole slots per thread");
-  __shared__ W2Lds<NW> L;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  const PatternArgs& p = a.pat;
-  const int lg = p.buckets_log2;
-  const int P = 1 << lg;
-  const int bucket = xcd_bucket(blockIdx.x, P);
-  const int kpb = (int)((p.key_capacity + P - 1) >> lg);
-  const int ntiles = a.ntiles;
-  const int64_t ks = a.kstride;
-  const int sw = p.slot_words;   // 2 + ncap
-  const int S = p.pending_slots;
-  const int64_t W = p.within;
-  const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
-  uint64_t ph_t = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
-
-  // ---- key lane (tid < kpb): pending count + slots 0 / 1 in registers
-  const bool klane = tid < kpb;
-  const int64_t kidx = (int64_t)bucket * kpb + tid;
-  const uint32_t kb = (uint32_t)kidx * 8u, pb = (uint32_t)ks * 8u;
-  auto sl_ld = [&](int j, int w) -> uint64_t {
-    return *(const uint64_t*)((const char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb));
-  };
-  auto sl_st = [&](int j, int w, uint64_t v) {
-    *(uint64_t*)((char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb)) = v;
-  };
-  uint32_t hdr = klane ? a.khdr[kidx] : 0u;
-  const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
-  const uint16_t* rhi = rlo + ntiles;
-  const int tb = tid * TPT;
-  auto load_tile_off = [&](const uint16_t* row, uint32_t (&o)[TPT / 2]) {
-    if ((ntiles & (TPT - 1)) == 0 && tb + TPT <= ntiles) {
-      if constexpr (TPT == 8) {
-        const uint4 x = *(const uint4*)(row + tb);
-        o[0] = x.x; o[1 % (TPT / 2)] = x.y; o[2 % (TPT / 2)] = x.z; o[3 % (TPT / 2)] = x.w;
-      } else {
-        const uint2 x = *(const uint2*)(row + tb);
-        o[0] = x.x; o[1 % (TPT / 2)] = x.y;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < TPT / 2; ++i) o[i] = 0;
-#pragma unroll
-      for (int i = 0; i < TPT; ++i) {
-        const int t = tb + i;
-        o[i >> 1] |= (t < ntiles ? (uint32_t)row[t] : 0u) << (16 * (i & 1));
-      }
-    }
-  };
-  uint32_t lop[TPT / 2], ys[TPT / 2];
-  load_tile_off(rlo, lop);
-  load_tile_off(rhi, ys);
-  int n = (int)(hdr & 0xffu);
-  const bool c1 = sw > 2, c2 = sw > 3;
-  uint64_t t0r = 0, t1r = 0, a0c0 = 0, a0c1 = 0, a1c0 = 0, a1c1 = 0;
-  bool dirty = false;
-  if (n > 0) {
-    t0r = sl_ld(0, 0);
-    if (c1) a0c0 = sl_ld(0, 2);
-    if (c2) a0c1 = sl_ld(0, 3);
-  }
-  if (n > 1) {
-    t1r = sl_ld(1, 0);
-    if (c1) a1c0 = sl_ld(1, 2);
-    if (c2) a1c1 = sl_ld(1, 3);
-  }
-  auto slot_word = [&](int j, int w) -> uint64_t {
-    if (j >= 2) return sl_ld(j, w);
-    const uint64_t m0 = 0ull - (uint64_t)(j == 0), m1 = ~m0;
-    const uint64_t w0 = 0ull - (uint64_t)(w == 0), w2 = 0ull - (uint64_t)(w == 2);
-    const uint64_t w3 = 0ull - (uint64_t)(w == 3);
-    return (m0 & ((t0r & w0) | (a0c0 & w2) | (a0c1 & w3))) | (m1 & ((t1r & w0) | (a1c0 & w2) | (a1c1 & w3)));
-  };
-  int nn = 0;
-  auto put_slot = [&](uint64_t ts, uint64_t x0, uint64_t x1) {
-    const uint64_t m0 = 0ull - (uint64_t)(nn == 0), m1 = 0ull - (uint64_t)(nn == 1);
-    t0r = (ts & m0) | (t0r & ~m0);
-    a0c0 = (x0 & m0) | (a0c0 & ~m0);
-    a0c1 = (x1 & m0) | (a0c1 & ~m0);
-    t1r = (ts & m1) | (t1r & ~m1);
-    a1c0 = (x0 & m1) | (a1c0 & ~m1);
-    a1c1 = (x1 & m1) | (a1c1 & ~m1);
-    if (nn >= 2) {   // slots 0 / 1 are stored once, at kernel end
-      sl_st(nn, 0, ts);
-      if (c1) sl_st(nn, 2, x0);
-      if (c2) sl_st(nn, 3, x1);
-    }
-    ++nn;
-    dirty = true;
-  };
-  const int64_t ts_base = a.chunk_base[0];
-  const int64_t seq_base = a.chunk_base[1];
-  auto seq_of = [&](uint32_t hs) -> int64_t {
-    return a.in_seq ? (int64_t)a.in_seq[(int64_t)hs * a.in_rec_words] : seq_base + (int64_t)hs;
-  };
-
-  // ---- the bucket's segment of every tile: exclusive prefix over tiles
-  // (this thread's first tile; the others follow from the segment sizes)
-  uint32_t spre0;
-  uint32_t nall;
-  {
-    uint32_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < TPT; ++i)
-      sum += ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - ((lop[i >> 1] >> (16 * (i & 1))) & 0xffffu);
-    spre0 = bscan<NT>(sum, L.scratch, &nall);
-  }
-  W2_PH(0);
-
-  for (uint32_t wb = 0; wb < nall; wb += WIN) {
-    const uint32_t nw = min((uint32_t)WIN, nall - wb);
-    // opaque per window: keeps the compiler from hoisting the per-tile
-    // values of step 1 out of the window loop (that many live registers spill)
-#pragma unroll
-    for (int i = 0; i < TPT / 2; ++i) asm volatile("" : "+v"(lop[i]), "+v"(ys[i]));
-    asm volatile("" : "+v"(spre0));
-    // ---- 1. window slot -> arena record index
-    uint32_t s0 = spre0;
-#pragma unroll
-    for (int i = 0; i < TPT; ++i) {
-      const uint32_t st = (lop[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-      const uint32_t c = ((ys[i >> 1] >> (16 * (i & 1))) & 0xffffu) - st;
-      const uint32_t lo = max(s0, wb), hi = min(s0 + c, wb + nw);
-      const uint32_t g0 = (uint32_t)(tb + i) * (uint32_t)kCfTile + st;
-      for (uint32_t g = lo; g < hi; ++g) L.wrec[g - wb] = g0 + (g - s0);
-      s0 += c;
-    }
-    L.wk[wave].kcur[lane] = 0;
-    lds_barrier();
-    W2_PH(1);
-
-    // ---- 2. gather (wave w: slots [w * 64 * PER, (w + 1) * 64 * PER), arrival
-    // order (i, lane)); stable rank per key group inside the wave
-    uint4 x[PER];
-    uint64_t y[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const uint32_t q = (uint32_t)(wave * 64 * PER + i * 64 + lane);
-      x[i] = make_uint4(0, 0, 0, 0);
-      y[i] = 0;
-      if (q < nw) {
-        const uint64_t* r = a.recs + (int64_t)L.wrec[q] * RW;
-        x[i] = gload4(r);
-        if (NW > 1) y[i] = r[2];
-      }
-    }
-    uint32_t gpos[PER];
-    {
-      uint32_t cnt[8];
-#pragma unroll
-      for (int g = 0; g < 8; ++g) cnt[g] = 0;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t q = (uint32_t)(wave * 64 * PER + i * 64 + lane);
-        const bool v = q < nw;
-        const uint32_t grp = (x[i].y >> 16) >> 6;
-        if (v) L.wrec[q] = (L.wrec[q] & ~(uint32_t)(kCfTile - 1)) + rec_row(((uint64_t)x[i].y << 32));
-        gpos[i] = 0;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          const uint64_t m = __ballot(v && grp == (uint32_t)g);
-          if (v && grp == (uint32_t)g) gpos[i] = cnt[g] + (uint32_t)__popcll(m & lt);
-          cnt[g] += (uint32_t)__popcll(m);
-        }
-      }
-      uint32_t mine = 0;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) mine = lane == g ? cnt[g] : mine;
-      if (lane < 8) L.gcnt[wave][lane] = mine;
-    }
-    lds_barrier();
-    W2_PH(2);
-
-    // ---- 3. group regions: (group, wave)-major offsets from one wave scan
-    uint32_t gs, gn;
-    {
-      const uint32_t gv = L.gcnt[lane & 7][lane >> 3];   // lane = group * 8 + wave
-      uint32_t inc = gv;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-      }
-      const uint32_t ex = inc - gv;
-      const uint32_t tot = __shfl(inc, 63, 64);
-      gs = __shfl(ex, wave * 8, 64);
-      gn = (wave < 7 ? __shfl(ex, wave * 8 + 8, 64) : tot) - gs;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t q = (uint32_t)(wave * 64 * PER + i * 64 + lane);
-        const uint32_t key = x[i].y >> 16;
-        const uint32_t pos = __shfl(ex, (int)((key >> 6) * 8 + wave), 64) + gpos[i];
-        if (q < nw) {
-          const uint32_t role = (x[i].y >> 13) & 7u;
-          L.gmeta[pos] = q | ((role & ROLE_A) ? 1u << 12 : 0u) | ((role & ROLE_B) ? 1u << 13 : 0u) |
-                         ((key & 63u) << 14);
-          L.gts[pos] = x[i].x;
-          if (NW > 0) L.gcap[0][pos] = ((uint64_t)x[i].w << 32) | x[i].z;
-          if (NW > 1) L.gcap[NW > 1 ? 1 : 0][pos] = y[i];
-        }
-      }
-    }
-    lds_barrier();
-    W2_PH(3);
-
-    // ---- 4a. per wave: stable counting sort of the group region by key
-    uint32_t kc, kst;
-    {
-      for (uint32_t c0 = 0; c0 < gn; c0 += 64) {
-        const uint32_t pp = c0 + lane;
-        const bool v = pp < gn;
-        const uint32_t k6 = v ? (L.gmeta[gs + pp] >> 14) & 63u : 0u;
-        const uint64_t m = peers6(k6, v);
-        if (v && (m & lt) == 0) L.wk[wave].kcur[k6] += (uint32_t)__popcll(m);
-      }
-      kc = L.wk[wave].kcur[lane];
-      uint32_t inc = kc;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-      }
-      kst = inc - kc;
-      L.wk[wave].kcur[lane] = kst;
-      for (uint32_t c0 = 0; c0 < gn; c0 += 64) {
-        const uint32_t pp = c0 + lane;
-        const bool v = pp < gn;
-        const uint32_t k6 = v ? (L.gmeta[gs + pp] >> 14) & 63u : 0u;
-        const uint64_t m = peers6(k6, v);
-        const uint32_t b = L.wk[wave].kcur[k6];
-        if (v && (m & lt) == 0) L.wk[wave].kcur[k6] = b + (uint32_t)__popcll(m);
-        if (v) L.sidx[gs + b + (uint32_t)__popcll(m & lt)] = (uint16_t)(gs + pp);
-      }
-    }
-    W2_PH(4);
-    // ---- 4b. right-to-left: next B of every sorted position, record matches
-    uint32_t amatch = 0;
-    {
-      L.wk[wave].kfb[lane] = (uint16_t)kW2None;
-      L.wk[wave].klb[lane] = (uint16_t)kW2None;
-      uint32_t cnb = kW2None, cts = 0;
-      const int nch = (int)((gn + 63) >> 6);
-      for (int ch = nch - 1; ch >= 0; --ch) {
-        const uint32_t c0 = (uint32_t)ch * 64u, sp = c0 + lane;
-        const bool v = sp < gn;
-        uint32_t meta = 0, dts = 0;
-        if (v) {
-          const uint32_t ri = L.sidx[gs + sp];
-          meta = L.gmeta[ri];
-          dts = L.gts[ri];
-        }
-        const uint32_t k6 = (meta >> 14) & 63u;
-        const bool isA = v && (meta & (1u << 12)), isB = v && (meta & (1u << 13));
-        // (every lane runs the shuffle: a lane outside the exec mask feeds 0)
-        const uint32_t kstk = (uint32_t)__shfl((int)kst, (int)k6, 64);
-        const bool sstart = v && sp == kstk;
-        const uint64_t Bm = __ballot(isB), Sm = __ballot(sstart);
-        const uint64_t ab = lanes_above(lane);
-        const int fb = (Bm & ab) ? __ffsll((long long)(Bm & ab)) - 1 : 64;
-        const int fs = (Sm & ab) ? __ffsll((long long)(Sm & ab)) - 1 : 64;
-        const uint32_t tnext = (uint32_t)__shfl((int)dts, fb < 64 ? fb : 0, 64);
-        uint32_t nb = kW2None, nbts = 0;
-        if (fb < fs) {
-          nb = c0 + (uint32_t)fb;
-          nbts = tnext;
-        } else if (fs == 64 && cnb != kW2None) {
-          nb = cnb;
-          nbts = cts;
-        }
-        bool match = false;
-        if (isA && nb != kW2None) {
-          const int64_t d = (int64_t)nbts - (int64_t)dts;
-          match = W < 0 || (d < 0 ? -d : d) <= W;
-        }
-        if (v) L.snb[gs + sp] = (uint16_t)(nb | (match ? kW2Match : 0u));
-        if (sstart) L.wk[wave].kfb[k6] = (uint16_t)(isB ? sp : nb);
-        if (isB && nb == kW2None) L.wk[wave].klb[k6] = (uint16_t)sp;
-        amatch += (uint32_t)__popcll(__ballot(match));
-        // carry into the chunk on the left: the first B of the run that
-        // continues across the chunk border, if any
-        const int fb0 = Bm ? __ffsll((long long)Bm) - 1 : 64;
-        const int fs0 = Sm ? __ffsll((long long)Sm) - 1 : 64;
-        const uint32_t t0 = (uint32_t)__shfl((int)dts, fb0 < 64 ? fb0 : 0, 64);
-        if (fs0 == 0) {
-          cnb = kW2None;
-        } else if (fb0 < fs0) {
-          cnb = c0 + (uint32_t)fb0;
-          cts = t0;
-        } else if (fs0 < 64) {
-          cnb = kW2None;
-        }
-      }
-    }
-    W2_PH(5);
-    // ---- key lanes: carried partials completed by the run's first B
-    const int kl = wave * 64 + lane;           // key in bucket
-    const bool hasrun = klane && kc > 0;
-    const uint32_t kfb = L.wk[wave].kfb[lane], klb = L.wk[wave].klb[lane];
-    int cfirst = n, cm = 0;
-    int64_t fbts = 0;
-    if (hasrun && kfb != kW2None && n > 0) {
-      fbts = ts_base + (int64_t)L.gts[L.sidx[gs + kfb]];
-      for (int j = 0; j < n; ++j) {
-        const int64_t d = fbts - (int64_t)slot_word(j, 0);
-        if (W < 0 || (d < 0 ? -d : d) <= W) {
-          cfirst = j;
-          break;
-        }
-      }
-      cm = n - cfirst;
-    }
-    uint32_t cmpre, cmw;
-    {
-      uint32_t inc = (uint32_t)cm;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-      }
-      cmpre = inc - (uint32_t)cm;
-      cmw = __shfl(inc, 63, 64);
-    }
-    if (lane == 0) L.wtot[wave] = cmw + amatch;
-    lds_barrier();
-    W2_PH(6);
-    if (tid == 0) {
-      uint32_t t = 0;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) t += L.wtot[w];
-      L.base = t ? atomicAdd(a.out.count, (unsigned long long)t) : 0ull;
-    }
-    lds_barrier();
-    W2_PH(7);
-    unsigned long long woff = L.base;
-    for (int w = 0; w < wave; ++w) woff += L.wtot[w];
-
-    // ---- 5a. key lanes: carried matches, new pending list (before the
-    // record emission: a slot read issued after a wave's output stores would
-    // wait for all of them)
-    if (hasrun) {
-      const int64_t kv = (((int64_t)kl << lg) | bucket) * p.key_stride + p.key_offset;
-      if (cm > 0) {
-        const uint32_t rib = L.sidx[gs + kfb];
-        const uint64_t b0 = NW > 0 ? L.gcap[0][rib] : 0ull, b1 = NW > 1 ? L.gcap[NW > 1 ? 1 : 0][rib] : 0ull;
-        const int64_t bseq = seq_of(L.wrec[L.gmeta[rib] & 0xfffu]);
-        for (int j = 0; j < cm; ++j) {
-          const int js = cfirst + j;
-          cf_emit(a, woff + cmpre + j, kv, c1 ? slot_word(js, 2) : 0ull, c2 ? slot_word(js, 3) : 0ull, b0, b1,
-                  fbts, bseq);
-        }
-      }
-      const uint32_t kend = kst + kc;
-      const uint32_t rl = L.sidx[gs + kend - 1];
-      const bool last_is_a = (L.gmeta[rl] >> 12) & 1u;
-      const int64_t last_a_ts = ts_base + (int64_t)L.gts[rl];
-      const bool prune = W >= 0 && last_is_a;
-      nn = 0;
-      if (kfb == kW2None) {   // no B in the run: the old list minus its pruned prefix
-        int drop = 0;
-        while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
-        if (drop == 0) {
-          nn = n;
-        } else {
-          for (int j = drop; j < n; ++j) {
-            const uint64_t ts = slot_word(j, 0);
-            const uint64_t x0 = c1 ? slot_word(j, 2) : 0ull, x1 = c2 ? slot_word(j, 3) : 0ull;
-            put_slot(ts, x0, x1);
-          }
-        }
-      }
-      // the run's A's from its last B on become pending (pruned; a record
-      // that is both B and A starts a partial after completing the others)
-      for (uint32_t sp = (kfb == kW2None ? kst : (uint32_t)klb); sp < kend; ++sp) {
-        const uint32_t ri = L.sidx[gs + sp];
-        if (!((L.gmeta[ri] >> 12) & 1u)) continue;
-        const int64_t ats = ts_base + (int64_t)L.gts[ri];
-        if (prune && last_a_ts - ats > W) continue;
-        if (nn >= S) {
-          set_err(a.err, ERR_PENDING);
-          break;
-        }
-        const uint64_t a0 = NW > 0 ? L.gcap[0][ri] : 0ull, a1 = NW > 1 ? L.gcap[NW > 1 ? 1 : 0][ri] : 0ull;
-        put_slot((uint64_t)ats, cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1),
-                 cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
-      }
-      dirty |= nn != n;
-      n = nn;
-      hdr = (hdr & ~0xffu) | (uint32_t)nn;
-    }
-
-    W2_PH(8);
-    // ---- 5b. record matches in (key, arrival) order
-    {
-      const unsigned long long o0 = woff + cmw;
-      uint32_t run = 0;
-      for (uint32_t c0 = 0; c0 < gn; c0 += 64) {
-        const uint32_t sp = c0 + lane;
-        const uint32_t f = sp < gn ? (uint32_t)L.snb[gs + sp] : 0u;
-        const bool match = (f & kW2Match) != 0;
-        const uint64_t m = __ballot(match);
-        if (match) {
-          const uint32_t ri = L.sidx[gs + sp], rib = L.sidx[gs + (f & kW2None)];
-          const uint32_t meta = L.gmeta[ri];
-          const int64_t ats = ts_base + (int64_t)L.gts[ri];
-          const int64_t bts = ts_base + (int64_t)L.gts[rib];
-          const uint64_t a0 = NW > 0 ? L.gcap[0][ri] : 0ull, a1 = NW > 1 ? L.gcap[NW > 1 ? 1 : 0][ri] : 0ull;
-          const uint64_t x0 = cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1);
-          const uint64_t x1 = cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1);
-          const int64_t key = (((int64_t)(wave * 64 + ((meta >> 14) & 63u)) << lg) | bucket) * p.key_stride +
-                              p.key_offset;
-          cf_emit(a, o0 + run + (uint32_t)__popcll(m & lt), key, x0, x1,
-                  NW > 0 ? L.gcap[0][rib] : 0ull, NW > 1 ? L.gcap[NW > 1 ? 1 : 0][rib] : 0ull, bts,
-                  seq_of(L.wrec[L.gmeta[rib] & 0xfffu]));
-        }
-        run += (uint32_t)__popcll(m);
-      }
-    }
-    lds_barrier();   // the window's LDS is rewritten by the next one
-    W2_PH(9);
-  }
-  // ---- the key's header and register-resident slots 0 / 1, once
-  if (klane && dirty) {
-    if (n > 0) {
-      sl_st(0, 0, t0r);
-      if (c1) sl_st(0, 2, a0c0);
-      if (c2) sl_st(0, 3, a0c1);
-    }
-    if (n > 1) {
-      sl_st(1, 0, t1r);
-      if (c1) sl_st(1, 2, a1c0);
-      if (c2) sl_st(1, 3, a1c1);
-    }
-    a.khdr[kidx] = hdr;
-  }
-  W2_PH(10);
-}
-
-bool cf_walk2_selected() {   // read per launch: tests switch it inside one process
-  const char* e = std::getenv("CEP_WALK");
-  return e && std::atoi(e) == 2;
-}
-
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
-  if (!cf_walk2_selected()) {
-    switch (a.cf.nw) {
-      case 0: hipLaunchKernelGGL(k_cfwalk<0>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-      case 1: hipLaunchKernelGGL(k_cfwalk<1>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-      default: hipLaunchKernelGGL(k_cfwalk<2>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-    }
-    return;
-  }
   switch (a.cf.nw) {
-    case 0: hipLaunchKernelGGL(k_cfwalk2<0>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-    case 1: hipLaunchKernelGGL(k_cfwalk2<1>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-    default: hipLaunchKernelGGL(k_cfwalk2<2>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
+    case 0: hipLaunchKernelGGL(k_cfwalk<0>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
+    case 1: hipLaunchKernelGGL(k_cfwalk<1>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_cfwalk<2>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
   }
 }
 

@@ -580,7 +580,6 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     pa.tile_off = (uint16_t*)rt.cf_toff[b].p;
     pa.ntiles = (int32_t)ntiles;
     pa.err = (unsigned int*)a->err.p;
-    pa.stable = cf_walk2_selected() ? 1 : 0;
     if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
     if (overlap && rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
     {
@@ -843,15 +842,6 @@ void cep_destroy(cep_app* a) {
         for (int i = 11; i < 16; ++i)
           if (t[i] && t[i - 1]) sum[i] += (double)(t[i] - t[i - 1]);
       }
-    }
-    if (cf_walk2_selected()) {
-      // k_cfwalk2: cycles per phase summed over each block's windows
-      double sum2[16] = {0};
-      for (int b = 0; b < nb; ++b)
-        for (int i = 0; i < 11; ++i) sum2[i] += (double)st[(size_t)b * 16 + i];
-      std::fprintf(stderr, "[cep stamps] walk2 cycles/block:");
-      for (int i = 0; i < 11; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum2[i] / nb);
-      std::fprintf(stderr, "\n");
     }
     std::fprintf(stderr, "[cep stamps] walk window0 ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);

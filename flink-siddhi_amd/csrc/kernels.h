@@ -225,7 +225,6 @@ struct CfPartArgs {
   uint16_t* tile_off;          // out: [P+1][ntiles] exclusive bucket offsets, bucket-major
   int32_t ntiles;
   uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per tile 16 s_memtime stamps
-  int32_t stable;              // 1: bucket segments in arrival order (k_cfwalk2 needs it)
   unsigned int* err;
 };
 
@@ -258,7 +257,6 @@ struct CfRouteArgs {
 // --------------------------------------------------------------- launchers --
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
-bool cf_walk2_selected();   // CEP_WALK=2: k_cfwalk2 instead of k_cfwalk
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

@@ -23,17 +23,13 @@ from flink_siddhi import _lib as L  # noqa: E402
 from flink_siddhi import workload  # noqa: E402
 
 
-@pytest.fixture(params=["cf", "cf2", "general"])
+@pytest.fixture(params=["cf", "general"])
 def path(request, monkeypatch):
-    """cf: k_cfpart + k_cfwalk; cf2: k_cfpart (arrival-ordered segments) +
-    k_cfwalk2 (CEP_WALK=2); general: k_partition + k_walk (CEP_NO_CF=1)."""
-    monkeypatch.delenv("CEP_WALK", raising=False)
+    """cf: k_cfpart + k_cfwalk; general: k_partition + k_walk (CEP_NO_CF=1)."""
     if request.param == "general":
         monkeypatch.setenv("CEP_NO_CF", "1")
     else:
         monkeypatch.delenv("CEP_NO_CF", raising=False)
-        if request.param == "cf2":
-            monkeypatch.setenv("CEP_WALK", "2")
     return request.param
 
 
@@ -55,7 +51,7 @@ def check_path(rt, path):
     st = rt.stats()
     cf = st.kernel_launches[L.K_CF_WALK]
     gen = st.kernel_launches[L.K_WALK]
-    if path in ("cf", "cf2"):
+    if path == "cf":
         assert cf > 0 and gen == 0, (cf, gen)
     else:
         assert cf == 0 and gen > 0, (cf, gen)

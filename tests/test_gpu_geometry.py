@@ -79,9 +79,7 @@ def assert_same_per_key(got, want):
                                  "(key %d)" % (c, i, a[i], b[i], int(want["k"][ow][i])))
 
 
-@pytest.mark.parametrize("walk", ["1", "2"])
-def test_config3_bench_geometry(walk, monkeypatch):
-    monkeypatch.setenv("CEP_WALK", walk)   # k_cfwalk (default) / k_cfwalk2
+def test_config3_bench_geometry():
     sizes = [CHUNK + 777, CHUNK - 777, 1 << 24]
     out, st = run_engine(sizes)
     n = sum(sizes)
