@@ -641,8 +641,15 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     *(uint64_t*)((char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb)) = v;
   };
   uint32_t hdr = klane ? a.khdr[kidx] : 0u;
-
-  // ---- the bucket's segment in every tile: two contiguous rows of the
+  // A pending list longer than the S inline slots keeps slots [S, n) in an
+  // overflow run of the pending pool: header bit kHdrOvf set, kext = n |
+  // run offset << 32 in this launch's read pool.  Runs are rewritten into the
+  // write pool whenever the list is rebuilt (and moved there at kernel end
+  // otherwise): the host swaps the two pools per launch.
+  const bool ovf0 = klane && (hdr & kHdrOvf);
+  uint64_t ext = ovf0 ? a.kext[kidx] : 0ull;
+  const uint64_t* ov = ovf0 ? a.pool_rd + (ext >> 32) * (uint64_t)p.slot_words : nullptr;
+  bool ov_wr = false;   // the overflow run lives in the write pool
   // bucket-major offset table, loaded before the slot loads below (those
   // wait for hdr; these need not)
   const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   load_tile_off(rlo, lop);
   load_tile_off(rhi, ys);
 
-  int n = (int)(hdr & 0xffu);
+  int n = ovf0 ? (int)(uint32_t)ext : (int)(hdr & 0xffu);
   // Slots 0 / 1 (ts + captures) live in registers for the whole kernel: read
   // once here, rewritten by the commit of each window (named scalars: a
   // dynamically indexed array lands in scratch).  Word 1 of a slot (the A's
@@ -702,6 +709,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   uint32_t pcb = 0;
   auto slot_word = [&](int j, int w) -> uint64_t {
     if (j >= 2) {
+      if (j >= S) return ov[(int64_t)(j - S) * sw + w];
       if (j - 2 < cn) return L.pcache[pcb + (uint32_t)((j - 2) * cw + (w == 0 ? 0 : w - 1))];
       return sl_ld(j, w);
     }
@@ -901,19 +909,20 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     cn = 0;
     uint64_t pv0[2], pv1[2], pv2[2];
     uint32_t pco = 0;
-    const bool fill = klane && n > 2 && L.kstart[tid + 1] > L.kstart[tid];
+    const int ni = min(n, S);   // inline slots in use (overflow slots are read from the pool)
+    const bool fill = klane && ni > 2 && L.kstart[tid + 1] > L.kstart[tid];
     if (fill) {
-      const uint32_t need = (uint32_t)((n - 2) * cw);
+      const uint32_t need = (uint32_t)((ni - 2) * cw);
       pco = atomicAdd(&L.pc_used, need);
       if (pco + need <= (uint32_t)(WIN / 2)) {
         pcb = pco;
-        cn = n - 2;
+        cn = ni - 2;
       }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int j = 2 + u;
-      const bool ld = cn > 0 && j < n;
+      const bool ld = cn > 0 && j < ni;
       pv0[u] = ld ? sl_ld(j, 0) : 0ull;
       pv1[u] = (ld && c1) ? sl_ld(j, 2) : 0ull;
       pv2[u] = (ld && c2) ? sl_ld(j, 3) : 0ull;
@@ -954,7 +963,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (2 + u < n) put_pc(2 + u, pv0[u], pv1[u], pv2[u]);
-      for (int j = 4; j < n; ++j)   // long lists (rare)
+      for (int j = 4; j < ni; ++j)   // long lists (rare)
         put_pc(j, sl_ld(j, 0), c1 ? sl_ld(j, 2) : 0ull, c2 ? sl_ld(j, 3) : 0ull);
     }
     lds_barrier();
@@ -1057,6 +1066,23 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       // minus pruned ones.  Slot j is written only after every old slot it
       // could overwrite has been read (old slot j' >= j is read at step j').
       int nn = 0;
+      // capacity of the new list: the kept old entries + every record from
+      // the run's last B on; past S the tail goes to a fresh overflow run in
+      // the write pool (rare: a key with more than S live partials)
+      const uint32_t from = (lb == kNoB ? r0 : (uint32_t)lb);
+      int cap = (lb == kNoB ? n : 0) + (int)(r1 - from);
+      uint64_t* nov = nullptr;
+      unsigned long long noff = 0;
+      if (cap > S) {
+        const unsigned long long cnt = (unsigned long long)(cap - S);
+        noff = atomicAdd(a.pool_cursor, cnt);
+        if (noff + cnt > a.pool_cap) {
+          set_err(a.err, ERR_POOL);
+          cap = S;
+        } else {
+          nov = a.pool_wr + noff * (uint64_t)sw;
+        }
+      }
       auto put_slot = [&](uint64_t ts, uint64_t x0, uint64_t x1) {
         const uint64_t m0 = 0ull - (uint64_t)(nn == 0), m1 = 0ull - (uint64_t)(nn == 1);
         t0r = (ts & m0) | (t0r & ~m0);
@@ -1066,7 +1092,16 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         a1c0 = (x0 & m1) | (a1c0 & ~m1);
         a1c1 = (x1 & m1) | (a1c1 & ~m1);
         if (nn >= 2) CF_COUNT(4, 1);
-        if (nn >= 2) {   // slots 0 / 1 are stored once, at kernel end
+        if (nn >= S) {   // overflow run
+          if (!nov) {   // the pool ran out (ERR_POOL set): keep the device safe
+            ++nn;
+            return;
+          }
+          uint64_t* o = nov + (int64_t)(nn - S) * sw;
+          o[0] = ts;
+          if (c1) o[2] = x0;
+          if (c2) o[3] = x1;
+        } else if (nn >= 2) {   // slots 0 / 1 are stored once, at kernel end
           sl_st(nn, 0, ts);
           if (c1) sl_st(nn, 2, x0);
           if (c2) sl_st(nn, 3, x1);
@@ -1079,7 +1114,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       } else if (lb == kNoB) {
         int drop = 0;
         while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
-        if (drop == 0) {
+        if (drop == 0 && cap <= S) {
           nn = n;   // unchanged, in place
         } else {
           if (n > 2) CF_COUNT(3, 1);
@@ -1096,8 +1131,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         if (!((L.skr[q] >> 12) & ROLE_A)) continue;
         const int64_t ats = ts_base + (int64_t)L.sts[q];
         if (prune && last_a_ts - ats > W) continue;
-        if (nn >= S) {
-          set_err(a.err, ERR_PENDING);
+        if (nn >= cap) {   // only after the pool ran out (ERR_POOL is set)
+          set_err(a.err, ERR_POOL);
           break;
         }
         const uint64_t a0 = NW > 0 ? L.scap[0][q] : 0ull, a1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][q] : 0ull;
@@ -1105,8 +1140,15 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
                  cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
       }
       dirty |= nn != n;
+      if (nn > S) {
+        ov = nov;
+        ov_wr = true;
+        ext = (uint64_t)(uint32_t)nn | (noff << 32);
+      } else if (nn != n || n > S) {
+        ov = nullptr;
+        ov_wr = false;
+      }
       n = nn;
-      hdr = (hdr & ~0xffu) | (uint32_t)nn;
     }
     CF_STAMP(wi * 8 + 6);
 
@@ -1150,8 +1192,24 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
     lds_barrier();
   }
+  // ---- an overflow run still in the read pool moves to the write pool
+  // (the read pool is the next launch's write pool)
+  if (klane && n > S && !ov_wr) {
+    const unsigned long long cnt = (unsigned long long)(n - S);
+    const unsigned long long off = atomicAdd(a.pool_cursor, cnt);
+    if (off + cnt > a.pool_cap) {
+      set_err(a.err, ERR_POOL);
+    } else {
+      uint64_t* o = a.pool_wr + off * (uint64_t)sw;
+      for (int64_t i = 0; i < (int64_t)cnt * sw; ++i) o[i] = ov[i];
+      ext = (uint64_t)(uint32_t)n | (off << 32);
+      dirty = true;
+    }
+  }
   // ---- the key's header and register-resident slots 0 / 1, once
   if (klane && dirty) {
+    hdr = (hdr & ~(0xffu | kHdrOvf)) | (n > S ? ((uint32_t)S | kHdrOvf) : (uint32_t)n);
+    if (n > S) a.kext[kidx] = ext;
     if (n > 0) {
       sl_st(0, 0, t0r);
       if (c1) sl_st(0, 2, a0c0);

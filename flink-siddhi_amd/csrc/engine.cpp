@@ -92,6 +92,11 @@ struct PatternRT {
   bool cf = false;
   int64_t cf_chunk = 0;
   DevBuf cf_recs[2], cf_toff[2];
+  // pending lists longer than S (closed-form path): per-key count + run
+  // offset, and two pools of overflow slots swapped per walk launch
+  DevBuf kext, pool[2], pool_cur;
+  int pool_side = 0;           // pool[pool_side] holds the current runs
+  int64_t pool_cap = 0;        // slots per pool
 };
 
 struct TimedLaunch {
@@ -413,7 +418,7 @@ int create_runtime(cep_app* a) {
     {
       bool ok = p.closed_form && !q.nfa && !agg && !rt.part_vm && !rt.walk_vm && rt.pref.n >= 0 &&
                 p.ncap <= kCfMaxCaps && p.nrec_a <= kPfRec && p.nrec_b <= kPfRec &&
-                kpb <= kCfMaxKeys && (1 << lg) <= kCfMaxBuckets && !std::getenv("CEP_NO_CF") &&
+                kpb <= kCfMaxKeys && (1 << lg) <= kCfMaxBuckets && !std::getenv("CEP_NO_CF") && S >= 2 &&
                 (double)rt.kstride * S * p.slot_words * 8 < 4294967296.0;   // 32-bit slot offsets
       ok = ok && (int)q.select.size() <= kCfMaxOut;
       for (auto& it : q.select)
@@ -429,6 +434,15 @@ int create_runtime(cep_app* a) {
           ok = dev_ensure(&rt.cf_recs[b], (size_t)cc * rw * 8 + 16, a->stream, false) &&
                dev_ensure(&rt.cf_toff[b], (size_t)nt * ((1 << lg) + 1) * 2 + 16, a->stream, false);
         if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
+        const int plg = a->opt.pending_pool_log2 > 0 ? std::min(a->opt.pending_pool_log2, 30) : 20;
+        rt.pool_cap = (int64_t)1 << plg;
+        ok = dev_ensure(&rt.kext, (size_t)rt.kstride * 8, a->stream, false) &&
+             dev_ensure(&rt.pool[0], (size_t)rt.pool_cap * p.slot_words * 8, a->stream, false) &&
+             dev_ensure(&rt.pool[1], (size_t)rt.pool_cap * p.slot_words * 8, a->stream, false) &&
+             dev_ensure(&rt.pool_cur, 64, a->stream, false);
+        if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (pending pool)");
+        hipMemset(rt.kext.p, 0, (size_t)rt.kstride * 8);
+        rt.extra_bound += rt.pool_cap;   // pool partials may complete too
         rt.cf = true;
         rt.cf_chunk = cc;
       }
@@ -600,6 +614,12 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     wa.khdr = (uint32_t*)rt.khdr.p;
     wa.kslot = (uint64_t*)rt.kslot.p;
     wa.kstride = rt.kstride;
+    wa.kext = (uint64_t*)rt.kext.p;
+    wa.pool_rd = (const uint64_t*)rt.pool[rt.pool_side].p;
+    wa.pool_wr = (uint64_t*)rt.pool[rt.pool_side ^ 1].p;
+    wa.pool_cursor = (unsigned long long*)rt.pool_cur.p;
+    wa.pool_cap = (uint64_t)rt.pool_cap;
+    hipMemsetAsync(rt.pool_cur.p, 0, 8, a->stream);
     wa.out = out_args(o, q);
     wa.err = pa.err;
     wa.in_seq = in_recs ? in_recs + rows.row0 * in_rec_words + 1 : nullptr;
@@ -614,6 +634,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       LaunchTimer t(a, CEP_K_CF_WALK);
       launch_cf_walk(wa, P, a->stream);
     }
+    rt.pool_side ^= 1;   // this launch's write pool holds every run now
     if (overlap) hipEventRecord(rt.walk_done[b], a->stream);
     rt.used[b] = true;
   }
@@ -726,6 +747,8 @@ int check_device_error(cep_app* a) {
     return fail(a, CEP_E_ARG, "events not in event-time order: `within` requires non-decreasing timestamps");
   if (e & ERR_PENDING)
     return fail(a, CEP_E_CAPACITY, "per-key pending partial capacity exceeded (raise pending_slots)");
+  if (e & ERR_POOL)
+    return fail(a, CEP_E_CAPACITY, "pending overflow pool exhausted (raise pending_pool_log2)");
   if (e & ERR_KEY_RANGE)
     return fail(a, CEP_E_CAPACITY, "partition key outside [0, key_capacity) or not owned by this shard");
   if (e & ERR_OUT_CAP) return fail(a, CEP_E_DEVICE, "output capacity exceeded");
@@ -748,6 +771,7 @@ void cep_default_options(cep_options* o) {
   o->ordered_output = 1;
   o->key_stride = 1;
   o->key_offset = 0;
+  o->pending_pool_log2 = 20;
 }
 
 int cep_validate(const char* plan, char* err, size_t errlen) {
@@ -883,6 +907,10 @@ void cep_destroy(cep_app* a) {
   for (auto& p : a->pats) {
     dev_free(&p.khdr);
     dev_free(&p.kslot);
+    dev_free(&p.kext);
+    dev_free(&p.pool[0]);
+    dev_free(&p.pool[1]);
+    dev_free(&p.pool_cur);
     for (int b = 0; b < 2; ++b) {
       dev_free(&p.recs[b]);
       dev_free(&p.tile_off[b]);
@@ -1302,15 +1330,17 @@ const char* cep_last_error(cep_app* a) { return a ? a->last_error.c_str() : "nul
 
 void cep_free(void* p) { std::free(p); }
 
-// Snapshot format (little endian), version 3:
+// Snapshot format (little endian), version 4:
 //   "CEPS" u32 version, u64 plan_hash, i64 events_in, u32 n_patterns,
 //   per pattern: i64 key_capacity, u32 S, u32 slot_words, u32 n_live,
-//                n_live x { u32 key, u64 header, (header & 0xff) * slot_words u64 }
+//                n_live x { u32 key, u64 header, u32 n, n * slot_words u64 }
+//                (n = pending partials, inline slots then the overflow run;
+//                versions 2 / 3 have no n: n = header & 0xff)
 //   (version >= 3) the event-time reorder buffer ("queuedRecordsState",
 //   AbstractSiddhiOperator.java:98): i32 input (-1: empty), u8 has_stream,
 //   i64 n, i64 released_max, then n rows: every column of the input's
 //   definition (type width each), n x i64 ts, n x u8 stream if has_stream.
-// Version 2 (no reorder section) is still restored.
+// Versions 2 (no reorder section) and 3 are still restored.
 static uint64_t plan_hash(const CompiledApp& app) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](const void* p, size_t n) {
@@ -1332,7 +1362,7 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
   };
   const char magic[4] = {'C', 'E', 'P', 'S'};
   put(magic, 4);
-  uint32_t ver = 3;   // 3: + the event-time reorder buffer
+  uint32_t ver = 4;   // 3: + the event-time reorder buffer; 4: + pending counts (overflow runs)
   put(&ver, 4);
   uint64_t h = plan_hash(a->app);
   put(&h, 8);
@@ -1345,9 +1375,15 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
     const int lg = rt.pa.buckets_log2;
     const int64_t kpb = ks >> lg;
     std::vector<uint32_t> hdr(ks);
-    std::vector<uint64_t> slots((size_t)ks * S * sw);
+    std::vector<uint64_t> slots((size_t)ks * S * sw), ext, pool;
     hipMemcpy(hdr.data(), rt.khdr.p, hdr.size() * 4, hipMemcpyDeviceToHost);
     hipMemcpy(slots.data(), rt.kslot.p, slots.size() * 8, hipMemcpyDeviceToHost);
+    if (rt.kext.p) {
+      ext.resize(ks);
+      pool.resize((size_t)rt.pool_cap * sw);
+      hipMemcpy(ext.data(), rt.kext.p, ext.size() * 8, hipMemcpyDeviceToHost);
+      hipMemcpy(pool.data(), rt.pool[rt.pool_side].p, pool.size() * 8, hipMemcpyDeviceToHost);
+    }
     uint32_t live = 0;
     for (int64_t i = 0; i < ks; ++i) live += hdr[i] ? 1 : 0;
     put(&kc, 8);
@@ -1357,11 +1393,16 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
     for (int64_t i = 0; i < ks; ++i) {
       if (!hdr[i]) continue;
       const uint32_t key = (uint32_t)(((i % kpb) << lg) | (i / kpb));   // dense key
-      const uint64_t h64 = hdr[i];
+      const bool ovf = (hdr[i] & kHdrOvf) && !ext.empty();
+      const uint64_t h64 = hdr[i] & ~(uint64_t)kHdrOvf;
+      const uint32_t n = ovf ? (uint32_t)ext[i] : (hdr[i] & 0xff);
+      const uint64_t off = ovf ? ext[i] >> 32 : 0;
       put(&key, 4);
       put(&h64, 8);
-      for (uint32_t j = 0; j < (hdr[i] & 0xff); ++j)
-        for (uint32_t w = 0; w < sw; ++w) put(&slots[((size_t)j * sw + w) * ks + i], 8);
+      put(&n, 4);
+      for (uint32_t j = 0; j < n; ++j)
+        for (uint32_t w = 0; w < sw; ++w)
+          put(j < S ? &slots[((size_t)j * sw + w) * ks + i] : &pool[(off + j - S) * sw + w], 8);
     }
   }
   // rows waiting for a watermark (the operator checkpoints its PriorityQueue
@@ -1408,7 +1449,7 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   uint64_t h;
   int64_t ev;
   uint32_t np;
-  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || (ver != 2 && ver != 3) || !get(&h, 8) ||
+  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver < 2 || ver > 4 || !get(&h, 8) ||
       !get(&ev, 8) || !get(&np, 4))
     return fail(a, CEP_E_STATE, "not a libcep snapshot");
   if (h != plan_hash(a->app) || np != a->pats.size())
@@ -1417,7 +1458,8 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   // device changes until the whole snapshot is known to be good.
   struct PatState {
     std::vector<uint32_t> hdr;
-    std::vector<uint64_t> slots;
+    std::vector<uint64_t> slots, ext, pool;
+    uint64_t pool_used = 0;
   };
   std::vector<PatState> ps(a->pats.size());
   for (size_t pi = 0; pi < a->pats.size(); ++pi) {
@@ -1435,17 +1477,39 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     const int64_t kpb = ks >> lg;
     ps[pi].hdr.assign(ks, 0);
     ps[pi].slots.assign((size_t)ks * S * sw, 0);
+    if (rt.kext.p) ps[pi].ext.assign(ks, 0);
     for (uint32_t i = 0; i < live; ++i) {
-      uint32_t key;
+      uint32_t key, nk;
       uint64_t h64;
-      if (!get(&key, 4) || !get(&h64, 8) || key >= kc || (h64 & 0xff) > S)
+      if (!get(&key, 4) || !get(&h64, 8) || key >= kc || (h64 & kHdrOvf))
         return fail(a, CEP_E_STATE, "corrupt snapshot");
+      if (ver >= 4) {
+        if (!get(&nk, 4)) return fail(a, CEP_E_STATE, "truncated snapshot");
+      } else {
+        nk = (uint32_t)(h64 & 0xff);
+      }
+      if ((uint64_t)nk * sw > (len - off) / 8) return fail(a, CEP_E_STATE, "truncated snapshot");
       const int64_t idx = (int64_t)(key & ((1u << lg) - 1)) * kpb + (key >> lg);
-      ps[pi].hdr[idx] = (uint32_t)h64;
-      for (uint32_t j = 0; j < (h64 & 0xff); ++j)
-        for (uint32_t w = 0; w < sw; ++w)
-          if (!get(&ps[pi].slots[((size_t)j * sw + w) * ks + idx], 8))
-            return fail(a, CEP_E_STATE, "truncated snapshot");
+      uint32_t hw = (uint32_t)h64;
+      if (nk > S) {   // overflow run: the pending pool (closed-form runtimes only)
+        if (ps[pi].ext.empty())
+          return fail(a, CEP_E_CAPACITY, "snapshot holds more than pending_slots partials for a key");
+        if (ps[pi].pool_used + (nk - S) > (uint64_t)rt.pool_cap)
+          return fail(a, CEP_E_CAPACITY, "snapshot's overflow partials exceed the pending pool");
+        ps[pi].ext[idx] = (uint64_t)nk | (ps[pi].pool_used << 32);
+        ps[pi].pool.resize((ps[pi].pool_used + (nk - S)) * sw);
+        hw = (hw & ~0xffu) | (uint32_t)S | kHdrOvf;
+      } else {
+        hw = (hw & ~0xffu) | nk;
+      }
+      for (uint32_t j = 0; j < nk; ++j)
+        for (uint32_t w = 0; w < sw; ++w) {
+          uint64_t* dst = j < S ? &ps[pi].slots[((size_t)j * sw + w) * ks + idx]
+                                : &ps[pi].pool[(ps[pi].pool_used + j - S) * sw + w];
+          if (!get(dst, 8)) return fail(a, CEP_E_STATE, "truncated snapshot");
+        }
+      if (nk > S) ps[pi].pool_used += nk - S;
+      ps[pi].hdr[idx] = hw;
     }
   }
   int32_t in = -1;
@@ -1478,8 +1542,14 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   }
   hipStreamSynchronize(a->stream);
   for (size_t pi = 0; pi < a->pats.size(); ++pi) {
-    hipMemcpy(a->pats[pi].khdr.p, ps[pi].hdr.data(), ps[pi].hdr.size() * 4, hipMemcpyHostToDevice);
-    hipMemcpy(a->pats[pi].kslot.p, ps[pi].slots.data(), ps[pi].slots.size() * 8, hipMemcpyHostToDevice);
+    PatternRT& rt = a->pats[pi];
+    hipMemcpy(rt.khdr.p, ps[pi].hdr.data(), ps[pi].hdr.size() * 4, hipMemcpyHostToDevice);
+    hipMemcpy(rt.kslot.p, ps[pi].slots.data(), ps[pi].slots.size() * 8, hipMemcpyHostToDevice);
+    if (rt.kext.p) {
+      hipMemcpy(rt.kext.p, ps[pi].ext.data(), ps[pi].ext.size() * 8, hipMemcpyHostToDevice);
+      if (!ps[pi].pool.empty())
+        hipMemcpy(rt.pool[rt.pool_side].p, ps[pi].pool.data(), ps[pi].pool.size() * 8, hipMemcpyHostToDevice);
+    }
   }
   r.n = 0;
   r.input = -1;

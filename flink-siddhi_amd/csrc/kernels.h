@@ -54,7 +54,13 @@ enum : uint32_t {
   ERR_ORDER = 4u,            // ts decreased inside a batch (within needs event-time order)
   ERR_OUT_CAP = 8u,          // output capacity exceeded (engine sizing bug)
   ERR_WINDOW = 16u,          // bucket window logic error
+  ERR_POOL = 32u,            // pending overflow pool exhausted
 };
+
+// Per-key state header: pending count (bits 0-7, <= S) | started << 8 |
+// kHdrOvf: the list is longer than S and continues in the pending pool
+// (closed-form path only; kext = count | pool run offset << 32).
+constexpr uint32_t kHdrOvf = 1u << 9;
 
 // ---------------------------------------------------------------- filter --
 struct FilterArgs {
@@ -238,6 +244,11 @@ struct CfWalkArgs {
   uint32_t* khdr;              // per-key state, same layout as WalkArgs
   uint64_t* kslot;
   int64_t kstride;
+  uint64_t* kext;              // per key: count | overflow run offset << 32 (header bit kHdrOvf)
+  const uint64_t* pool_rd;     // pending pool this launch reads overflow runs from
+  uint64_t* pool_wr;           // ... and writes rebuilt runs to (slot s word w at [s * slot_words + w])
+  unsigned long long* pool_cursor;   // slots allocated in pool_wr (zeroed per launch)
+  uint64_t pool_cap;           // slots per pool
   OutArgs out;
   const uint64_t* in_seq;      // received records: &record[row0].seq (global arrival numbers), else nullptr
   int32_t in_rec_words;

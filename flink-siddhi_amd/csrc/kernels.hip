@@ -1290,7 +1290,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
   const int64_t seq_base = a.chunk_base[1];
   const int64_t ks = a.kstride;
   // this bucket's per-key headers: kpb consecutive words (bucket-major index)
-  for (int k = tid; k < kpb; k += kWalkThreads) L.khdr[k] = a.khdr[(int64_t)bucket * kpb + k];
+  for (int k = tid; k < kpb; k += kWalkThreads) {
+    const uint32_t h = a.khdr[(int64_t)bucket * kpb + k];
+    // a list that overflowed into the pending pool (closed-form path) does
+    // not fit this walk's per-key LDS lists
+    if (h & kHdrOvf) set_err(a.err, ERR_PENDING);
+    L.khdr[k] = h & ~kHdrOvf;
+  }
 
   // segment starts and sizes -> exclusive prefix over tiles
   {

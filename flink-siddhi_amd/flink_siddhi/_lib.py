@@ -95,7 +95,8 @@ class cep_options(C.Structure):
                 ("key_capacity", C.c_int64), ("chunk_events", C.c_int64),
                 ("buckets_log2", C.c_int32), ("profile", C.c_int32),
                 ("ordered_output", C.c_int32), ("key_stride", C.c_int32),
-                ("key_offset", C.c_int32), ("reserved", C.c_int32 * 7)]
+                ("key_offset", C.c_int32), ("pending_pool_log2", C.c_int32),
+                ("reserved", C.c_int32 * 6)]
 
 
 class cep_batch(C.Structure):

@@ -54,6 +54,22 @@ def generate(first: int, n: int, keys: int, rate: int = 400, seed: int = SEED,
     return {"k": key, "stream": stream, "id": idv, "price": price, "ts": ts}
 
 
+def zipf_map(keys: int, s: float = 1.1, seed: int = 7):
+    """Zipf(s) over `keys` ranks as a key -> key remap of the uniform
+    generator's keys (BASELINE.md §3 "Zipf s=1.1 variant"): key k (uniform in
+    [0, keys)) becomes perm[rank], rank = the Zipf inverse CDF at (k + 0.5) /
+    keys; perm scatters the hot ranks over the key space (and so over
+    buckets).  Returns the int32 lookup table (numpy): zipf_key = table[k]."""
+    r = np.arange(1, keys + 1, dtype=np.float64)
+    w = r ** -s
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    u = (np.arange(keys, dtype=np.float64) + 0.5) / keys
+    rank = np.minimum(np.searchsorted(cdf, u, side="left"), keys - 1)
+    perm = np.random.default_rng(seed).permutation(keys).astype(np.int32)
+    return perm[rank]
+
+
 def _lsr(x, s: int):
     """Logical right shift of int64 tensors (torch's >> is arithmetic)."""
     return (x >> s) & ((1 << (64 - s)) - 1)

@@ -50,7 +50,7 @@ extern "C" {
  *   CEP_E_DEVICE           -> HIP failure / no gfx950 device
  *   CEP_E_CAPACITY         -> per-key pending-state or key-space capacity
  *                             exceeded (raise cep_options.pending_slots /
- *                             key_capacity)
+ *                             pending_pool_log2 / key_capacity)
  *   CEP_E_STATE            -> snapshot incompatible with this plan
  */
 enum {
@@ -90,7 +90,10 @@ typedef struct cep_options {
                               order; 0: per-key order (default 1) */
   int32_t key_stride;      /* multi-GPU: this shard owns keys with key % key_stride == key_offset (default 1/0) */
   int32_t key_offset;
-  int32_t reserved[7];
+  int32_t pending_pool_log2;  /* pending partials beyond pending_slots per key spill to a
+                                 device pool of 2^n slots (default 20); closed-form
+                                 patterns only, others fail with CEP_E_CAPACITY */
+  int32_t reserved[6];
 } cep_options;
 
 /* Fill *opt with defaults. */

@@ -166,14 +166,56 @@ def test_snapshot_cf_restore_general(monkeypatch):
     assert_same_rows(first + second, want, "cf snapshot -> general restore")
 
 
-def test_pending_overflow_reported(path):
+def test_pending_lists_longer_than_pending_slots(path):
+    """Siddhi's pending list is unbounded.  64 keys, B's rare (g: id % 25 ==
+    0): runs of ~13 f-passing A's per key between g-passing B's, often more
+    than pending_slots = 16 (SURVEY §7 "unbounded pending lists").  The
+    closed-form path spills the tail to the pending pool and matches the
+    oracle; the general path has per-key LDS lists and reports capacity."""
+    w = workload.generate(0, 60000, 64, rate=1)
+    plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id % 25 == 0")
+    if path == "general":
+        rt = fs.SiddhiAppRuntime(plan, pending_slots=16)
+        rt.add_callback("O")
+        rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
+        with pytest.raises(fs.CepCapacityError):
+            rt.flush()
+        rt.shutdown()
+        return
+    assert case(plan, w, path, batches=3, chunk_events=16384, pending_slots=16) > 500
+
+
+def test_pending_pool_exhausted_is_reported():
     w = workload.generate(0, 30000, 64, rate=1)
-    plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id == 1000")
-    rt = fs.SiddhiAppRuntime(plan, pending_slots=16)
+    plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id == 1000")   # no B: lists only grow
+    rt = fs.SiddhiAppRuntime(plan, pending_slots=4, pending_pool_log2=6)
     rt.add_callback("O")
     rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
-    with pytest.raises(fs.CepCapacityError):
+    with pytest.raises(fs.CepCapacityError, match="pool"):
         rt.flush()
+    rt.shutdown()
+
+
+def test_overflow_snapshot_restore():
+    """Overflow runs survive snapshot / restore (snapshot v4 carries the
+    pending count and every partial)."""
+    w = workload.generate(0, 60000, 64, rate=1)
+    plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id % 25 == 0")
+    want = oracle_run(plan, workload_events(w)).get("O", [])
+    h = 31000
+    rt = fs.SiddhiAppRuntime(plan, pending_slots=4)
+    rt.add_callback("O")
+    send_all(rt, {k: v[:h] for k, v in w.items()})
+    first = engine_rows(rt.collect("O"))
+    snap = rt.snapshot()
+    rt.shutdown()
+    rt2 = fs.SiddhiAppRuntime(plan, pending_slots=4)
+    rt2.add_callback("O")
+    rt2.restore(snap)
+    send_all(rt2, {k: v[h:] for k, v in w.items()})
+    second = engine_rows(rt2.collect("O"))
+    rt2.shutdown()
+    assert_same_rows(first + second, want, "overflow snapshot/restore")
 
 
 def test_fast_path_engaged_on_config3_device_batch():

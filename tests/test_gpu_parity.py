@@ -222,9 +222,12 @@ def test_device_resident_batch_matches_host_batch():
     assert_same_rows(got, want, "device vs host batch")
 
 
-def test_pending_overflow_is_reported():
+def test_pending_overflow_general_path_is_reported(monkeypatch):
     # g never holds: every key keeps ~39 live partials inside the 10 s window
-    # (64 keys, 1 event/ms), more than 16 slots
+    # (64 keys, 1 event/ms), more than 16 slots.  The general walk keeps
+    # per-key lists in LDS and reports capacity (the closed-form path spills
+    # to the pending pool: test_gpu_cf.py::test_pending_lists_longer_than_pending_slots)
+    monkeypatch.setenv("CEP_NO_CF", "1")
     w = workload.generate(0, 30000, 64, rate=1)
     plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id == 1000")
     rt = fs.SiddhiAppRuntime(plan, pending_slots=16)

@@ -234,10 +234,23 @@ def test_restore_version2_snapshot():
     first = engine_rows(rt.collect("O"))
     snap = bytearray(rt.snapshot())
     rt.shutdown()
-    assert struct.unpack_from("<I", snap, 4)[0] == 3
-    # empty reorder section: i32 input, u8 has_stream, i64 n, i64 released_max
-    v2 = snap[:-21]
+    assert struct.unpack_from("<I", snap, 4)[0] == 4
+    # version 2 layout: no per-key pending count, no reorder section (an
+    # empty one is i32 input, u8 has_stream, i64 n, i64 released_max)
+    v2 = bytearray(snap[:28])
     struct.pack_into("<I", v2, 4, 2)
+    off = 28
+    for _ in range(struct.unpack_from("<I", snap, 24)[0]):
+        kc, S, sw, live = struct.unpack_from("<qIII", snap, off)
+        v2 += snap[off:off + 20]
+        off += 20
+        for _ in range(live):
+            key, hdr, n = struct.unpack_from("<IQI", snap, off)
+            assert n == hdr & 0xff
+            v2 += snap[off:off + 12]
+            v2 += snap[off + 16:off + 16 + n * sw * 8]
+            off += 16 + n * sw * 8
+    assert len(snap) - off == 21
     rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
     rt2.add_callback("O")
     rt2.restore(bytes(v2))
