@@ -592,7 +592,7 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
     const int src = a.out.src[c];
     uint64_t v;
     if (src == SRC_KEY) {
-      v = (uint64_t)key;
+      v = a.key_rev ? a.key_rev[key] : (uint64_t)key;
     } else if (src >= SRC_CAP && src < SRC_REC) {
       v = (src - SRC_CAP) == 0 ? acap0 : acap1;
     } else {

@@ -97,6 +97,10 @@ struct PatternRT {
   DevBuf kext, pool[2], pool_cur;
   int pool_side = 0;           // pool[pool_side] holds the current runs
   int64_t pool_cap = 0;        // slots per pool
+  // sparse partition keys (cep_options.sparse_keys): value -> dense slot map
+  bool sparse = false;
+  uint64_t table_cap = 0;
+  DevBuf tkey, tval, krev, kcount, dense;
 };
 
 struct TimedLaunch {
@@ -447,6 +451,32 @@ int create_runtime(cep_app* a) {
         rt.cf_chunk = cc;
       }
     }
+    if (a->opt.sparse_keys && keyed) {
+      // the map feeds the closed-form path's key column: the key may appear
+      // in the plan only as the partition key (and `select s1.k`)
+      const PrefPlan& pf = rt.pref;
+      bool ok = rt.cf && a->opt.key_stride <= 1 && pf.key_slot == 0;
+      for (int i = 0; ok && i < q.f_terms.n; ++i) ok = pf.f_slot[i] != 0;
+      for (int i = 0; ok && i < q.g_terms.n; ++i) ok = pf.g_slot[i] != 0;
+      for (int i = 0; ok && i < p.nrec_a; ++i) ok = pf.reca_slot[i] != 0;
+      for (int i = 0; ok && i < p.nrec_b; ++i) ok = pf.recb_slot[i] != 0;
+      const int kt = app.inputs[q.a_stream].attrs[q.key_col_a].type;
+      ok = ok && (kt == T_INT || kt == T_LONG);
+      if (!ok)
+        return fail(a, CEP_E_UNSUPPORTED, "not supported: sparse_keys needs a closed-form `every A -> B` pattern whose int / long "
+                                          "partition key is used only as the key, on one shard");
+      uint64_t tc = 1;
+      while (tc < 2 * (uint64_t)kc) tc <<= 1;
+      rt.sparse = true;
+      rt.table_cap = tc;
+      if (!dev_ensure(&rt.tkey, tc * 8, a->stream, false) || !dev_ensure(&rt.tval, tc * 4, a->stream, false) ||
+          !dev_ensure(&rt.krev, (size_t)kc * 8, a->stream, false) || !dev_ensure(&rt.kcount, 64, a->stream, false))
+        return fail(a, CEP_E_DEVICE, "out of device memory (key map)");
+      hipMemset(rt.tkey.p, 0, tc * 8);
+      hipMemset(rt.tval.p, 0xff, tc * 4);
+      hipMemset(rt.kcount.p, 0, 4);
+      hipMemset((char*)rt.kcount.p + 4, 0xff, 4);
+    }
     a->pats.push_back(rt);
   }
   if (std::getenv("CEP_STAMPS") && !dev_ensure(&a->stamps, (size_t)2 * 4096 * 16 * 8, a->stream, false))
@@ -619,6 +649,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     wa.pool_wr = (uint64_t*)rt.pool[rt.pool_side ^ 1].p;
     wa.pool_cursor = (unsigned long long*)rt.pool_cur.p;
     wa.pool_cap = (uint64_t)rt.pool_cap;
+    wa.key_rev = rt.sparse ? (const uint64_t*)rt.krev.p : nullptr;
     hipMemsetAsync(rt.pool_cur.p, 0, 8, a->stream);
     wa.out = out_args(o, q);
     wa.err = pa.err;
@@ -649,6 +680,44 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
   o.bound += rows_all.n;
   int rc = ensure_out_cap(a, o, o.bound);
   if (rc) return rc;
+  if (rt.sparse) {
+    // partition values -> dense slots (keymap.hip); the pattern then reads
+    // the dense column in place of the key column
+    if (in_recs) return fail(a, CEP_E_UNSUPPORTED, "sparse_keys with the multi-GPU key shuffle");
+    const int kcol = rows_all.input == q.b_stream ? q.key_col_b : q.key_col_a;
+    if (!dev_ensure(&rt.dense, (size_t)std::max<int64_t>(rows_all.n, 1) * 4 + 16, a->stream, false))
+      return fail(a, CEP_E_DEVICE, "out of device memory (dense keys)");
+    KeyMapArgs ka{};
+    ka.key = rows_all.cols.p[kcol];
+    ka.key_is_long = rows_all.cols.t[kcol] == T_LONG ? 1 : 0;
+    ka.stream = rows_all.stream;
+    ka.input = rows_all.input;
+    ka.a_stream = q.a_stream;
+    ka.b_stream = q.b_stream;
+    ka.row0 = rows_all.row0;
+    ka.n = rows_all.n;
+    ka.tkey = (unsigned long long*)rt.tkey.p;
+    ka.tval = (uint32_t*)rt.tval.p;
+    ka.table_cap = rt.table_cap;
+    ka.rev = (uint64_t*)rt.krev.p;
+    ka.count = (unsigned int*)rt.kcount.p;
+    ka.minus_one = (unsigned int*)rt.kcount.p + 1;
+    ka.cap = (uint32_t)rt.pa.key_capacity;
+    ka.out = (int32_t*)rt.dense.p;
+    ka.err = (unsigned int*)a->err.p;
+    {
+      LaunchTimer t(a, CEP_K_OTHER);
+      launch_keymap(ka, a->stream);
+    }
+    RowsArgs rows = rows_all;
+    // the dense column is indexed from the slice's first row
+    rows.cols.p[kcol] = (const int32_t*)rt.dense.p - rows_all.row0;
+    rows.cols.t[kcol] = T_INT;
+    CfPlan cf;
+    if (!pref_aligned(rt.pref, rows) || !cf_plan(rt, rows, &cf, false))
+      return fail(a, CEP_E_ARG, "sparse_keys needs 16-byte aligned columns");
+    return run_pattern_cf(a, rt, q, o, rows, cf);
+  }
   if (rt.cf && (in_recs || pref_aligned(rt.pref, rows_all))) {
     CfPlan cf;
     if (cf_plan(rt, rows_all, &cf, in_recs != nullptr))
@@ -749,6 +818,8 @@ int check_device_error(cep_app* a) {
     return fail(a, CEP_E_CAPACITY, "per-key pending partial capacity exceeded (raise pending_slots)");
   if (e & ERR_POOL)
     return fail(a, CEP_E_CAPACITY, "pending overflow pool exhausted (raise pending_pool_log2)");
+  if (e & ERR_KEYMAP)
+    return fail(a, CEP_E_CAPACITY, "more distinct partition values than key_capacity (sparse_keys)");
   if (e & ERR_KEY_RANGE)
     return fail(a, CEP_E_CAPACITY, "partition key outside [0, key_capacity) or not owned by this shard");
   if (e & ERR_OUT_CAP) return fail(a, CEP_E_DEVICE, "output capacity exceeded");
@@ -911,6 +982,7 @@ void cep_destroy(cep_app* a) {
     dev_free(&p.pool[0]);
     dev_free(&p.pool[1]);
     dev_free(&p.pool_cur);
+    for (DevBuf* b : {&p.tkey, &p.tval, &p.krev, &p.kcount, &p.dense}) dev_free(b);
     for (int b = 0; b < 2; ++b) {
       dev_free(&p.recs[b]);
       dev_free(&p.tile_off[b]);
@@ -1339,7 +1411,9 @@ void cep_free(void* p) { std::free(p); }
 //   (version >= 3) the event-time reorder buffer ("queuedRecordsState",
 //   AbstractSiddhiOperator.java:98): i32 input (-1: empty), u8 has_stream,
 //   i64 n, i64 released_max, then n rows: every column of the input's
-//   definition (type width each), n x i64 ts, n x u8 stream if has_stream.
+//   definition (type width each), n x i64 ts, n x u8 stream if has_stream;
+//   (version 4) per pattern: u8 sparse keys, if set u32 count, u32 id of
+//   the value -1 (0xffffffff: none), count x i64 partition value per dense slot.
 // Versions 2 (no reorder section) and 3 are still restored.
 static uint64_t plan_hash(const CompiledApp& app) {
   uint64_t h = 1469598103934665603ull;
@@ -1427,6 +1501,19 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
       pull(r.ts, (size_t)r.n * 8);
       if (r.has_stream) pull(r.stream, (size_t)r.n);
     }
+  }
+  // (version 4) per pattern: the sparse-key map, dense slot -> value
+  for (auto& rt : a->pats) {
+    const uint8_t sp = rt.sparse ? 1 : 0;
+    put(&sp, 1);
+    if (!sp) continue;
+    uint32_t cnt[2];
+    hipMemcpy(cnt, rt.kcount.p, 8, hipMemcpyDeviceToHost);
+    cnt[0] = std::min<uint32_t>(cnt[0], (uint32_t)rt.pa.key_capacity);
+    put(cnt, 8);
+    std::vector<uint64_t> rev(cnt[0]);
+    if (cnt[0]) hipMemcpy(rev.data(), rt.krev.p, rev.size() * 8, hipMemcpyDeviceToHost);
+    put(rev.data(), rev.size() * 8);
   }
   *buf = (uint8_t*)std::malloc(out.size());
   if (!*buf) return fail(a, CEP_E_DEVICE, "out of host memory");
@@ -1526,7 +1613,45 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
       if ((uint64_t)n > (len - off) / row_bytes)
         return fail(a, CEP_E_STATE, "truncated snapshot (reorder buffer)");
       rows_off = off;
+      off += (size_t)n * row_bytes;
     }
+  }
+  // sparse-key maps: rebuilt here as device tables (same hash and probing
+  // as keymap.hip; any valid placement serves lookups)
+  struct KeyMap {
+    std::vector<uint64_t> tkey, rev;
+    std::vector<uint32_t> tval;
+    uint32_t cnt[2] = {0, 0xffffffffu};
+  };
+  std::vector<KeyMap> km(a->pats.size());
+  if (ver >= 4) {
+    for (size_t pi = 0; pi < a->pats.size(); ++pi) {
+      const PatternRT& rt = a->pats[pi];
+      uint8_t sp;
+      if (!get(&sp, 1) || (sp != 0) != rt.sparse) return fail(a, CEP_E_STATE, "snapshot key map does not match");
+      if (!sp) continue;
+      KeyMap& m = km[pi];
+      if (!get(m.cnt, 8) || m.cnt[0] > (uint64_t)rt.pa.key_capacity || (uint64_t)m.cnt[0] > (len - off) / 8)
+        return fail(a, CEP_E_STATE, "corrupt snapshot (key map)");
+      m.rev.resize(m.cnt[0]);
+      get(m.rev.data(), m.rev.size() * 8);
+      m.tkey.assign(rt.table_cap, 0);
+      m.tval.assign(rt.table_cap, 0xffffffffu);
+      for (uint32_t id = 0; id < m.cnt[0]; ++id) {
+        if (id == m.cnt[1]) continue;   // the value -1 has its own word
+        const uint64_t v = m.rev[id];
+        uint64_t z = v + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        uint64_t h = (z ^ (z >> 31)) & (rt.table_cap - 1);
+        while (m.tkey[h]) h = (h + 1) & (rt.table_cap - 1);
+        m.tkey[h] = v + 1;
+        m.tval[h] = id;
+      }
+    }
+  } else {
+    for (auto& rt : a->pats)
+      if (rt.sparse) return fail(a, CEP_E_STATE, "snapshot has no key map (version < 4)");
   }
   // Phase 2: commit (device allocations first, so a failure leaves the
   // runtime as it was)
@@ -1568,6 +1693,14 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     r.input = in;
     r.has_stream = hs != 0;
     r.n = n;
+  }
+  for (size_t pi = 0; pi < a->pats.size(); ++pi) {
+    PatternRT& rt = a->pats[pi];
+    if (!rt.sparse) continue;
+    hipMemcpy(rt.tkey.p, km[pi].tkey.data(), km[pi].tkey.size() * 8, hipMemcpyHostToDevice);
+    hipMemcpy(rt.tval.p, km[pi].tval.data(), km[pi].tval.size() * 4, hipMemcpyHostToDevice);
+    if (!km[pi].rev.empty()) hipMemcpy(rt.krev.p, km[pi].rev.data(), km[pi].rev.size() * 8, hipMemcpyHostToDevice);
+    hipMemcpy(rt.kcount.p, km[pi].cnt, 8, hipMemcpyHostToDevice);
   }
   a->events_in = ev;
   return CEP_OK;

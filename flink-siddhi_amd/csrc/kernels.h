@@ -55,6 +55,7 @@ enum : uint32_t {
   ERR_OUT_CAP = 8u,          // output capacity exceeded (engine sizing bug)
   ERR_WINDOW = 16u,          // bucket window logic error
   ERR_POOL = 32u,            // pending overflow pool exhausted
+  ERR_KEYMAP = 64u,          // more distinct partition values than key_capacity (sparse keys)
 };
 
 // Per-key state header: pending count (bits 0-7, <= S) | started << 8 |
@@ -249,6 +250,7 @@ struct CfWalkArgs {
   uint64_t* pool_wr;           // ... and writes rebuilt runs to (slot s word w at [s * slot_words + w])
   unsigned long long* pool_cursor;   // slots allocated in pool_wr (zeroed per launch)
   uint64_t pool_cap;           // slots per pool
+  const uint64_t* key_rev;     // sparse keys: dense key -> partition value (nullptr: dense keys)
   OutArgs out;
   const uint64_t* in_seq;      // received records: &record[row0].seq (global arrival numbers), else nullptr
   int32_t in_rec_words;
@@ -265,9 +267,28 @@ struct CfRouteArgs {
   int32_t ts_slot;             // prefetch slot whose column IS the event-ts buffer (-1: none)
 };
 
+// Sparse partition keys (keymap.hip): value -> dense key slot.
+struct KeyMapArgs {
+  const void* key;             // key column (int32 or int64), batch rows
+  int32_t key_is_long;
+  const uint8_t* stream;       // per-row input handle or nullptr
+  int32_t input, a_stream, b_stream;
+  int64_t row0, n;
+  unsigned long long* tkey;    // table: stored value + 1 (0 = empty)
+  uint32_t* tval;              // table: dense id
+  uint64_t table_cap;          // power of two
+  uint64_t* rev;               // dense id -> value
+  unsigned int* count;         // dense ids handed out
+  unsigned int* minus_one;     // dense id of the value -1 (0xffffffff: none yet)
+  uint32_t cap;                // key_capacity
+  int32_t* out;                // dense id per row (row i of the slice)
+  unsigned int* err;
+};
+
 // --------------------------------------------------------------- launchers --
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
+void launch_keymap(const KeyMapArgs& a, hipStream_t s);
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

@@ -93,7 +93,10 @@ typedef struct cep_options {
   int32_t pending_pool_log2;  /* pending partials beyond pending_slots per key spill to a
                                  device pool of 2^n slots (default 20); closed-form
                                  patterns only, others fail with CEP_E_CAPACITY */
-  int32_t reserved[6];
+  int32_t sparse_keys;     /* 1: partition values are any int / long (a device hash map
+                              assigns up to key_capacity dense slots; values come back
+                              unchanged in `select s1.k`); 0: ints in [0, key_capacity) */
+  int32_t reserved[5];
 } cep_options;
 
 /* Fill *opt with defaults. */

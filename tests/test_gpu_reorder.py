@@ -203,14 +203,16 @@ def test_restore_rejects_truncated_snapshot_and_keeps_state():
     snap = rt.snapshot()
     rt.shutdown()
     rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
-    for cut in (len(snap) - 1, len(snap) - held * 5, 30):
+    for cut in (len(snap) - 2, len(snap) - held * 5, 30):
         with pytest.raises(fs.CepStateError):
             rt2.restore(snap[:cut])
         assert rt2.buffered() == 0
     # a lying row count (n huge, bytes short) is refused too
     import struct
     body = bytearray(snap)
-    tail = len(body) - held * (4 + 8 + 4 + 8 + 8 + 1)    # columns k ts id price + event ts + stream
+    # reorder rows (columns k ts id price + event ts + stream), then the
+    # 1-byte key-map section of the one pattern
+    tail = len(body) - 1 - held * (4 + 8 + 4 + 8 + 8 + 1)
     n_off = tail - 8 - 8                                   # i64 n, i64 released_max precede the rows
     assert struct.unpack_from("<q", body, n_off)[0] == held
     struct.pack_into("<q", body, n_off, (1 << 31) - 1)
@@ -250,7 +252,7 @@ def test_restore_version2_snapshot():
             v2 += snap[off:off + 12]
             v2 += snap[off + 16:off + 16 + n * sw * 8]
             off += 16 + n * sw * 8
-    assert len(snap) - off == 21
+    assert len(snap) - off == 22   # empty reorder section + the key-map byte
     rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
     rt2.add_callback("O")
     rt2.restore(bytes(v2))
