@@ -13,6 +13,12 @@ the keys k % N == rank and processes N events per step (weak scaling).
 `--workload filter` runs configs[1] (config 2): `inputStream[price > 0.5 and
 id % 7 == 0] select *` over 10^8 events.
 
+`--workload config5` runs configs[4] (config 5) on the GPUs given: one app of
+64 queries — 32 `every s1=A[price > q/32], s2=B[id == q%50]+, s3=C[id ==
+(q+1)%50] within 10 sec` sequences under `partition with (k ...)` and 32
+`group by k having` aggregations — over three keyed streams, K = 2^20 keys,
+2^24 events per step.
+
 Before the timed region (N=1): a parity check — a fresh runtime processes the
 first step's events and the order-sensitive digest of its device output is
 compared with oracle/cep_oracle.c's digest over the same events ("parity" in
@@ -53,7 +59,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["pattern", "filter"], default="pattern")
+    ap.add_argument("--workload", choices=["pattern", "filter", "config5"], default="pattern")
     ap.add_argument("--events", type=int, default=0, help="events per step per GPU")
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--rate", type=int, default=400, help="events per ms")
@@ -62,8 +68,13 @@ def parse():
                     help="key buckets = 2^n (0: engine default, <= 512 keys per bucket)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity check")
-    ap.add_argument("--ingest", choices=["shuffle", "prepartitioned"], default="shuffle",
-                    help="multi-GPU pattern input: engine key shuffle over RCCL, or keyed upstream")
+    ap.add_argument("--ingest", choices=["shuffle", "prepartitioned", "host", "host-pageable"],
+                    default="shuffle",
+                    help="multi-GPU pattern input: engine key shuffle over RCCL, or keyed upstream; "
+                         "1 GPU: host = batches in pinned host memory fed over PCIe (host-pageable: "
+                         "ordinary host memory) instead of device-resident inputs")
+    ap.add_argument("--deliver", action="store_true",
+                    help="deliver every match to a host callback at each flush (pinned D2H)")
     return ap.parse_args()
 
 
@@ -250,6 +261,38 @@ def cpu_baseline_filter(w):
                       "%.2f s" % (n, dt)}
 
 
+# ---------------------------------------------------------------- config 5 --
+def config5_parity(args, opts, n_check=20000):
+    """The bench stream's first n_check events through a fresh runtime vs the
+    Python oracle (oracle/siddhi_oracle.py: sequences and aggregates are not
+    in the C restatement), every output stream row for row."""
+    import numpy as np
+    import flink_siddhi as fs
+    from flink_siddhi import workload
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    from helpers import engine_rows, oracle_run
+    plan = workload.config5_plan()
+    w = workload.generate(0, n_check, args.keys, rate=args.rate)
+    w["stream"] = workload.config5_streams(w["price"]).astype(np.uint8)
+    rt = fs.SiddhiAppRuntime(plan, **dict(opts, profile=0, ordered_output=1))
+    for o in workload.CONFIG5_OUTPUTS:
+        rt.add_callback(o)
+    rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
+    rt.flush()
+    got = {o: engine_rows(rt.collect(o)) for o in workload.CONFIG5_OUTPUTS}
+    rt.shutdown()
+    names = "ABC"
+    ev = [(names[s], t, (k, t, i, p)) for k, t, i, p, s in
+          zip(w["k"].tolist(), w["ts"].tolist(), w["id"].tolist(), w["price"].tolist(), w["stream"].tolist())]
+    want = oracle_run(plan, ev)
+    bad = [o for o in workload.CONFIG5_OUTPUTS if got[o] != want.get(o, [])]
+    rows = sum(len(v) for v in got.values())
+    return {"parity": "ok" if not bad else "MISMATCH", "events": n_check, "rows": rows,
+            "mismatched_outputs": bad[:8],
+            "checker": "oracle/siddhi_oracle.py (Python restatement), every output, emission order"}
+
+
 # ------------------------------------------------------------------- main --
 def main():
     args = parse()
@@ -260,7 +303,8 @@ def main():
 
     world, rank, local = dist_init(args)
     pattern = args.workload == "pattern"
-    n = args.events or ((1 << 28) if pattern else 100_000_000)
+    config5 = args.workload == "config5"
+    n = args.events or ((1 << 28) if pattern else (1 << 24) if config5 else 100_000_000)
     steps, warm = args.steps, args.warmup
 
     if pattern:
@@ -270,13 +314,20 @@ def main():
                     profile=PROFILE_EVERY, ordered_output=0)
         if args.buckets_log2:
             opts["buckets_log2"] = args.buckets_log2
+    elif config5:
+        plan = workload.config5_plan()
+        opts = dict(device=local, key_capacity=(args.keys + world - 1) // world, key_stride=world,
+                    key_offset=rank, pending_slots=4, profile=PROFILE_EVERY, ordered_output=0)
     else:
         plan = workload.FILTER_PLAN
         opts = dict(device=local, profile=PROFILE_EVERY, ordered_output=0)
 
     # parity + CPU baseline first (N=1): the host leg needs the same events
     parity, cpu, kept = None, None, None
-    if world == 1 and not (args.no_parity and args.no_cpu):
+    if config5:
+        if world == 1 and not args.no_parity:
+            parity = config5_parity(args, opts)
+    elif world == 1 and not (args.no_parity and args.no_cpu):
         if pattern:
             parity, w, kept = pattern_parity(args, n, opts)
             if not args.no_cpu:
@@ -297,20 +348,31 @@ def main():
     # "prepartitioned" — the input is already keyed upstream (Flink keyBy):
     # rank r draws only keys it owns, no exchange.
     shuffle_mode = pattern and world > 1 and args.ingest == "shuffle"
+    host_ingest = args.ingest in ("host", "host-pageable") and world == 1
     batches = []
     for s in range(warm + steps):
         first = (s * world + rank) * n
         d = workload.generate_device(first, n, args.keys, rate=args.rate,
                                      single_stream=not pattern, device="cuda")
         d["first"] = first
-        if pattern and world > 1 and not shuffle_mode:
+        if (pattern or config5) and world > 1 and not shuffle_mode:
             d["k"] = (d["k"] // world) * world + rank     # owned keys, same distribution
-        if not pattern:
+        if config5:
+            d["stream"] = workload.config5_streams(d["price"]).to(torch.uint8)
+        elif not pattern:
             d["name"] = torch.zeros(n, dtype=torch.int32, device="cuda")
+        if host_ingest:   # the batch lives in host memory; the engine stages it over PCIe
+            d = {c: (v.cpu().pin_memory() if args.ingest == "host" else v.cpu()).numpy()
+                 if hasattr(v, "cpu") else v for c, v in d.items()}
         batches.append(d)
     torch.cuda.synchronize()
 
     bufs = {}
+    delivered = [0]
+    if args.deliver:
+        outs = workload.CONFIG5_OUTPUTS if config5 else ["O"]
+        for o in outs:
+            rt.add_callback(o, lambda rows: delivered.__setitem__(0, delivered[0] + len(rows)), copy=False)
 
     def step(d):
         if shuffle_mode:
@@ -322,7 +384,7 @@ def main():
             recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get("recv"))
             bufs["recv"] = recv
             rt.send_records(recv, m, n)
-        elif pattern:
+        elif pattern or config5:
             rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
         else:
             rt.send("inputStream", d["ts"], [d["id"], d["name"], d["price"], d["ts"]])
@@ -377,6 +439,12 @@ def main():
                 total_bytes[k] += kern[k]["launches"] * keys_local * CF_STATE_BYTES
         if shuffle_mode:
             total_bytes["k_route"] = ev_total * PATTERN_IN_BYTES
+    elif config5:
+        # one pass over the 25 B/event the queries read, plus every output row
+        # (~36 B: key, two f64 / i64 values, ts, seq); per kernel: each of the
+        # 64 queries' partition passes re-reads the columns it needs
+        alg_per_event = PATTERN_IN_BYTES + 36 * m_per_event
+        total_bytes = {"k_partition": ev_total * PATTERN_IN_BYTES * 64}
     else:
         alg_per_event = FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event
         total_bytes = {"k_filter": ev_total * alg_per_event}
@@ -404,6 +472,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "frac": round(per_gpu_events * alg_per_event / 1e9 / HBM_PEAK_GBS, 4)}
 
+    in_b = PATTERN_IN_BYTES if (pattern or config5) else 4 + 4 + 8 + 8 + 8   # bytes per host event
     if rank == 0:
         out = {
             "metric": "matched-pattern events/sec (whole node) at 1/2/4/8 MI355X + % HBM roofline",
@@ -419,6 +488,11 @@ def main():
                                     if shuffle_mode else
                                    "pre-partitioned (keyed upstream)") if world > 1 else "local"}
                        if pattern else
+                       {"workload": "config5: 64 queries (32 every A, B+, C within 10 sec sequences with "
+                                    "id == q%50, 32 group-by/having aggregations), 3 keyed streams",
+                        "keys": args.keys, "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
+                        "parallelism": "key-sharded x%d (pre-partitioned)" % world}
+                       if config5 else
                        {"workload": "config2: inputStream[price > 0.5 and id % 7 == 0] select *",
                         "events_per_step_per_gpu": n, "parallelism": "replicas x%d" % world}),
             "matches_per_s": round(matches_total / dt_max, 1),
@@ -428,6 +502,10 @@ def main():
             "roofline_kernels": per_kernel,
             "kernels": kern,
             "parity": parity,
+            "host_io": ({"ingest": args.ingest, "bytes_in_per_event": in_b,
+                         "pcie_in_GBs": round(value * in_b / 1e9, 2),
+                         "delivered_rows": delivered[0] if args.deliver else None}
+                        if host_ingest or args.deliver else None),
             "cpu_baseline": cpu,
             "speedup_vs_cpu_baseline": round(value / cpu["value"], 1) if cpu else None,
         }

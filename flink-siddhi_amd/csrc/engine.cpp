@@ -57,6 +57,38 @@ void dev_free(DevBuf* b) {
   b->bytes = 0;
 }
 
+// Pinned (page-locked) host memory: DMA at PCIe speed, no driver bounce.
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+bool host_ensure(HostBuf* b, size_t bytes) {
+  if (b->bytes >= bytes && b->p) return true;
+  const size_t nb = std::max(bytes, b->bytes * 2);
+  if (b->p) hipHostFree(b->p);
+  b->p = nullptr;
+  b->bytes = 0;
+  if (hipHostMalloc(&b->p, nb, hipHostMallocDefault) != hipSuccess) return false;
+  b->bytes = nb;
+  return true;
+}
+
+void host_free(HostBuf* b) {
+  if (b->p) hipHostFree(b->p);
+  b->p = nullptr;
+  b->bytes = 0;
+}
+
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t at;
+  if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();   // pageable memory: clear the sticky lookup error
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
 struct OutStream {
   std::string id;
   std::vector<int> types;
@@ -67,9 +99,11 @@ struct OutStream {
   int64_t bound = 0;                     // upper bound of rows since last flush
   cep_emit_fn fn = nullptr;
   void* user = nullptr;
-  // host copies for callback delivery
-  std::vector<std::vector<uint8_t>> hcols;
-  std::vector<int64_t> hts, hseq;
+  // pinned host copies for callback delivery (D2H at PCIe speed)
+  std::vector<HostBuf> hcols;
+  HostBuf hts, hseq;
+  std::vector<std::vector<uint8_t>> sorted;   // ordered_output: rows permuted into emission order
+  std::vector<int64_t> sts, sseq;
 };
 
 struct PatternRT {
@@ -128,7 +162,17 @@ struct cep_app {
   DevBuf tile_state, ticket, err;
   DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
-  std::vector<DevBuf> stage;   // host-batch staging columns (+ts, +stream)
+  // host batches: two staging slots (pinned host arena + device arena); a
+  // batch's H2D copy runs on the copy stream while the previous batch's
+  // kernels run on the main stream
+  struct HostSlot {
+    HostBuf pinned;
+    DevBuf dev;
+    hipEvent_t dma_done = nullptr, free = nullptr;
+    bool used = false;
+  } hs[2];
+  int hs_next = 0;
+  hipStream_t copy = nullptr;
   // event-time reorder buffer (cep_buffer_batch / cep_watermark): rows of
   // one input layout since the last watermark, SoA in arrival order
   struct Reorder {
@@ -254,7 +298,8 @@ int create_runtime(cep_app* a) {
       hipStreamCreateWithFlags(&a->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&a->in_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&a->ext_ready, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&a->out_ready, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&a->out_ready, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&a->copy, hipStreamNonBlocking) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
@@ -991,7 +1036,18 @@ void cep_destroy(cep_app* a) {
       dev_free(&p.chunk_base[b]);
     }
   }
-  for (auto& s : a->stage) dev_free(&s);
+  if (a->copy) hipStreamSynchronize(a->copy);
+  for (auto& h : a->hs) {
+    host_free(&h.pinned);
+    dev_free(&h.dev);
+    if (h.dma_done) hipEventDestroy(h.dma_done);
+    if (h.free) hipEventDestroy(h.free);
+  }
+  for (auto& o : a->outs) {
+    for (auto& h : o.hcols) host_free(&h);
+    host_free(&o.hts);
+    host_free(&o.hseq);
+  }
   for (int c = 0; c < kMaxCols; ++c) {
     dev_free(&a->ro.col[c]);
     dev_free(&a->ro.out[c]);
@@ -1019,6 +1075,7 @@ void cep_destroy(cep_app* a) {
   if (a->ext_ready) hipEventDestroy(a->ext_ready);
   if (a->out_ready) hipEventDestroy(a->out_ready);
   if (a->side) hipStreamDestroy(a->side);
+  if (a->copy) hipStreamDestroy(a->copy);
   if (a->stream) hipStreamDestroy(a->stream);
   delete a;
 }
@@ -1053,7 +1110,11 @@ namespace {
 
 // Batch -> device rows (host batches are staged into device memory: the
 // PCIe-inclusive path).  Validates the handle and the column count.
-int batch_rows(cep_app* a, const cep_batch* b, RowsArgs* out) {
+// *slot: the host staging slot the batch went to (-1: device batch);
+// *direct: its columns are DMA'd straight from pinned caller memory.
+int batch_rows(cep_app* a, const cep_batch* b, RowsArgs* out, int* slot, bool* direct) {
+  *slot = -1;
+  *direct = false;
   if (b->n < 0 || (b->n > 0 && !b->ts)) return fail(a, CEP_E_ARG, "bad batch");
   if (b->input < 0 || b->input >= (int)a->app.inputs.size())
     return fail(a, CEP_E_UNDEFINED_STREAM, "undefined input handle");
@@ -1077,27 +1138,59 @@ int batch_rows(cep_app* a, const cep_batch* b, RowsArgs* out) {
     // in-batch check covers the hot path
     a->last_ts = INT64_MIN;
   } else {
-    size_t need = (size_t)b->ncols + 2;
-    if (a->stage.size() < need) a->stage.resize(need);
-    for (int c = 0; c < b->ncols; ++c) {
-      size_t bytes = (size_t)b->n * type_width(sd.attrs[c].type);
-      if (!dev_ensure(&a->stage[c], bytes, a->stream, false))
+    // One staging slot holds the whole batch (columns, ts, stream; 256-B
+    // aligned pieces).  Pinned caller buffers are DMA'd directly; pageable
+    // ones are first copied by the CPU into the slot's pinned arena (that
+    // copy is the batch's consumption: the call returns without waiting for
+    // the device).  The DMA waits for the kernels that last read the slot.
+    auto& h = a->hs[a->hs_next];
+    *slot = a->hs_next;
+    a->hs_next ^= 1;
+    if (!h.dma_done && (hipEventCreateWithFlags(&h.dma_done, hipEventDisableTiming) != hipSuccess ||
+                        hipEventCreateWithFlags(&h.free, hipEventDisableTiming) != hipSuccess))
+      return fail(a, CEP_E_DEVICE, "hipEventCreate failed");
+    const int nc = b->ncols;
+    size_t off[kMaxCols + 2], len[kMaxCols + 2];
+    const void* src[kMaxCols + 2];
+    size_t total = 0;
+    auto piece = [&](int i, const void* p, size_t bytes) {
+      off[i] = total;
+      len[i] = bytes;
+      src[i] = p;
+      total += (bytes + 255) & ~(size_t)255;
+    };
+    for (int c = 0; c < nc; ++c) piece(c, b->cols[c], (size_t)b->n * type_width(sd.attrs[c].type));
+    piece(nc, b->ts, (size_t)b->n * 8);
+    piece(nc + 1, b->stream, b->stream ? (size_t)b->n : 0);
+    bool pinned = true;
+    for (int i = 0; i < nc + 2 && pinned; ++i) pinned = !len[i] || is_pinned(src[i]);
+    // the slot's previous DMA (two batches ago) must be done before its
+    // pinned arena or device arena is rewritten
+    if (h.used) hipEventSynchronize(h.dma_done);
+    if (h.dev.bytes < total) {
+      if (h.used) hipStreamSynchronize(a->stream);   // the old arena may still be read
+      if (!dev_ensure(&h.dev, total, a->stream, false))
         return fail(a, CEP_E_DEVICE, "out of device memory (staging)");
-      hipMemcpyAsync(a->stage[c].p, b->cols[c], bytes, hipMemcpyHostToDevice, a->stream);
-      rows.cols.p[c] = a->stage[c].p;
     }
-    DevBuf& tsb = a->stage[b->ncols];
-    if (!dev_ensure(&tsb, (size_t)b->n * 8, a->stream, false))
-      return fail(a, CEP_E_DEVICE, "out of device memory (staging)");
-    hipMemcpyAsync(tsb.p, b->ts, (size_t)b->n * 8, hipMemcpyHostToDevice, a->stream);
-    rows.ts = (const int64_t*)tsb.p;
-    if (b->stream) {
-      DevBuf& sb = a->stage[b->ncols + 1];
-      if (!dev_ensure(&sb, (size_t)b->n, a->stream, false))
-        return fail(a, CEP_E_DEVICE, "out of device memory (staging)");
-      hipMemcpyAsync(sb.p, b->stream, (size_t)b->n, hipMemcpyHostToDevice, a->stream);
-      rows.stream = (const uint8_t*)sb.p;
+    if (!pinned) {
+      if (!host_ensure(&h.pinned, total)) return fail(a, CEP_E_DEVICE, "out of pinned host memory");
+      for (int i = 0; i < nc + 2; ++i)
+        if (len[i]) std::memcpy((char*)h.pinned.p + off[i], src[i], len[i]);
     }
+    if (h.used) hipStreamWaitEvent(a->copy, h.free, 0);   // kernels done with the device arena
+    if (!pinned) {
+      hipMemcpyAsync(h.dev.p, h.pinned.p, total, hipMemcpyHostToDevice, a->copy);
+    } else {
+      for (int i = 0; i < nc + 2; ++i)
+        if (len[i]) hipMemcpyAsync((char*)h.dev.p + off[i], src[i], len[i], hipMemcpyHostToDevice, a->copy);
+    }
+    hipEventRecord(h.dma_done, a->copy);
+    hipStreamWaitEvent(a->stream, h.dma_done, 0);
+    h.used = true;
+    *direct = pinned;
+    for (int c = 0; c < nc; ++c) rows.cols.p[c] = (char*)h.dev.p + off[c];
+    rows.ts = (const int64_t*)((char*)h.dev.p + off[nc]);
+    rows.stream = b->stream ? (const uint8_t*)((char*)h.dev.p + off[nc + 1]) : nullptr;
     a->last_ts = b->ts[b->n - 1];
   }
   *out = rows;
@@ -1111,12 +1204,19 @@ int cep_send_batch(cep_app* a, const cep_batch* b) {
   if (!a->enabled) return CEP_OK;   // AbstractSiddhiOperator.java:128
   if (b->n == 0) return CEP_OK;
   RowsArgs rows{};
-  int rc = batch_rows(a, b, &rows);
+  int slot;
+  bool direct;
+  int rc = batch_rows(a, b, &rows, &slot, &direct);
   if (rc) return rc;
   a->events_in += b->n;
   a->batches++;
   rc = send_device_rows(a, rows);
-  if (b->on_device == 0) hipStreamSynchronize(a->stream);   // host buffers may be reused
+  if (slot >= 0) {
+    hipEventRecord(a->hs[slot].free, a->stream);
+    // caller's pinned buffers: consumed once their DMA is done (the kernels
+    // keep running); pageable buffers were consumed by the staging memcpy
+    if (direct) hipEventSynchronize(a->hs[slot].dma_done);
+  }
   return rc;
 }
 
@@ -1259,48 +1359,50 @@ int cep_flush(cep_app* a) {
     if (rc == CEP_OK) hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
     a->matches_out += (int64_t)cnt;
     if (o.fn && cnt > 0 && rc == CEP_OK) {
+      // one async D2H per column into pinned buffers, one sync
       const size_t n = cnt;
       o.hcols.resize(o.cols.size());
+      bool ok = host_ensure(&o.hts, n * 8) && host_ensure(&o.hseq, n * 8);
+      for (size_t c = 0; c < o.cols.size() && ok; ++c) ok = host_ensure(&o.hcols[c], n * type_width(o.types[c]));
+      if (!ok) return fail(a, CEP_E_DEVICE, "out of pinned host memory (output delivery)");
+      hipMemcpyAsync(o.hts.p, o.ts.p, n * 8, hipMemcpyDeviceToHost, a->stream);
+      hipMemcpyAsync(o.hseq.p, o.seq.p, n * 8, hipMemcpyDeviceToHost, a->stream);
+      for (size_t c = 0; c < o.cols.size(); ++c)
+        hipMemcpyAsync(o.hcols[c].p, o.cols[c].p, n * type_width(o.types[c]), hipMemcpyDeviceToHost, a->stream);
+      if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "output delivery failed");
+      const int64_t* hts = (const int64_t*)o.hts.p;
+      const int64_t* hseq = (const int64_t*)o.hseq.p;
       std::vector<const void*> ptrs(o.cols.size());
-      o.hts.resize(n);
-      o.hseq.resize(n);
-      hipMemcpy(o.hts.data(), o.ts.p, n * 8, hipMemcpyDeviceToHost);
-      hipMemcpy(o.hseq.data(), o.seq.p, n * 8, hipMemcpyDeviceToHost);
-      for (size_t c = 0; c < o.cols.size(); ++c) {
-        o.hcols[c].resize(n * type_width(o.types[c]));
-        hipMemcpy(o.hcols[c].data(), o.cols[c].p, o.hcols[c].size(), hipMemcpyDeviceToHost);
-      }
-      if (a->opt.ordered_output) {
+      for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.hcols[c].p;
+      if (a->opt.ordered_output && !std::is_sorted(hseq, hseq + n)) {
         // Siddhi's emission order: by completing event, then by pending
         // order (contiguous per key already) — a stable sort on seq.
         std::vector<uint32_t> perm(n);
         std::iota(perm.begin(), perm.end(), 0u);
-        bool sorted = std::is_sorted(o.hseq.begin(), o.hseq.end());
-        if (!sorted) {
-          std::stable_sort(perm.begin(), perm.end(),
-                           [&](uint32_t x, uint32_t y) { return o.hseq[x] < o.hseq[y]; });
-          auto apply = [&](std::vector<uint8_t>& col, int w) {
-            std::vector<uint8_t> tmp(col.size());
-            for (size_t i = 0; i < n; ++i) std::memcpy(&tmp[i * w], &col[(size_t)perm[i] * w], w);
-            col.swap(tmp);
-          };
-          for (size_t c = 0; c < o.cols.size(); ++c) apply(o.hcols[c], type_width(o.types[c]));
-          std::vector<int64_t> t2(n), s2(n);
-          for (size_t i = 0; i < n; ++i) {
-            t2[i] = o.hts[perm[i]];
-            s2[i] = o.hseq[perm[i]];
-          }
-          o.hts.swap(t2);
-          o.hseq.swap(s2);
+        std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return hseq[x] < hseq[y]; });
+        o.sorted.resize(o.cols.size());
+        for (size_t c = 0; c < o.cols.size(); ++c) {
+          const int w = type_width(o.types[c]);
+          o.sorted[c].resize(n * w);
+          const uint8_t* src = (const uint8_t*)o.hcols[c].p;
+          for (size_t i = 0; i < n; ++i) std::memcpy(&o.sorted[c][i * w], src + (size_t)perm[i] * w, w);
+          ptrs[c] = o.sorted[c].data();
         }
+        o.sts.resize(n);
+        o.sseq.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+          o.sts[i] = hts[perm[i]];
+          o.sseq[i] = hseq[perm[i]];
+        }
+        hts = o.sts.data();
+        hseq = o.sseq.data();
       }
-      for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.hcols[c].data();
       cep_rows rows{};
       rows.stream_id = o.id.c_str();
       rows.n = (int64_t)n;
       rows.ncols = (int32_t)o.cols.size();
-      rows.ts = o.hts.data();
-      rows.seq = o.hseq.data();
+      rows.ts = hts;
+      rows.seq = hseq;
       rows.cols = ptrs.data();
       o.fn(o.user, &rows);
     }
@@ -1728,7 +1830,9 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   if (!rec_out || rec_cap < b->n)
     return fail(a, CEP_E_ARG, "rec_out must hold at least n records (" + std::to_string(b->n) + ")");
   RowsArgs rows{};
-  int rc = batch_rows(a, b, &rows);
+  int slot;
+  bool direct;
+  int rc = batch_rows(a, b, &rows, &slot, &direct);
   if (rc) return rc;
   // fast route (k_cfroute) when every column the pattern reads is prefetchable
   // and f / g are term lists (the k_cfpart load path); CEP_NO_CF=1 forces k_route
@@ -1772,6 +1876,7 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
                    (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
     }
   }
+  if (slot >= 0) hipEventRecord(a->hs[slot].free, a->stream);
   std::vector<unsigned long long> dc(world);
   hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, a->stream);
   if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "route failed");

@@ -116,23 +116,26 @@ class SiddhiAppRuntime:
 
     # -- callbacks -------------------------------------------------------------
     def add_callback(self, out_id: str,
-                     fn: Optional[Callable[[OutputRows], None]] = None):
+                     fn: Optional[Callable[[OutputRows], None]] = None, copy: bool = True):
         """addCallback(outId, StreamCallback) (AbstractSiddhiOperator.java:165-166).
-        Without `fn`, rows are collected and returned by `collect(out_id)`."""
+        Without `fn`, rows are collected and returned by `collect(out_id)`.
+        copy=False hands `fn` views of the engine's (pinned) delivery buffers,
+        valid only during the call."""
         types = [t for _, t in self.stream_definition(out_id)]
         self._collected.setdefault(out_id, [])
 
         def cb(user, rows_p):
             r = rows_p.contents
             n = r.n
-            ts = np.ctypeslib.as_array(r.ts, shape=(n,)).copy() if n else np.zeros(0, np.int64)
-            seq = np.ctypeslib.as_array(r.seq, shape=(n,)).copy() if n else np.zeros(0, np.int64)
+            cp = (lambda x: x.copy()) if copy or fn is None else (lambda x: x)
+            ts = cp(np.ctypeslib.as_array(r.ts, shape=(n,))) if n else np.zeros(0, np.int64)
+            seq = cp(np.ctypeslib.as_array(r.seq, shape=(n,))) if n else np.zeros(0, np.int64)
             cols = []
             for c, t in enumerate(types):
                 dt = np.dtype(L.NUMPY_DTYPES[t])
                 if n:
                     buf = (C.c_char * (n * dt.itemsize)).from_address(r.cols[c])
-                    cols.append(np.frombuffer(buf, dtype=dt).copy())
+                    cols.append(cp(np.frombuffer(buf, dtype=dt)))
                 else:
                     cols.append(np.zeros(0, dt))
             out = OutputRows(out_id, ts, seq, cols)

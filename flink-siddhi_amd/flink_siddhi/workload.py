@@ -31,6 +31,35 @@ FILTER_PLAN = (
     "from inputStream[price > 0.5 and id % 7 == 0] select * insert into O;")
 
 
+def config5_plan() -> str:
+    """BASELINE config 5 exactly as SURVEY §8(d) states it, one app of 64
+    queries over three keyed streams: q = 0..31 `every s1=A[price > q/32],
+    s2=B[id == q%50]+, s3=C[id == (q+1)%50] within 10 sec` (outputs Seq<q>),
+    q = 32..63 `from A[price > (q-32)/32] select k, sum(price) as total,
+    count() as n group by k having total > 1.0` (outputs Agg<q>)."""
+    ev = "".join("define stream %s (k int, ts long, id int, price double);" % s for s in "ABC")
+    seq = ["partition with (k of A, k of B, k of C) begin "]
+    for q in range(32):
+        seq.append("from every s1=A[price > %s], s2=B[id == %d]+, s3=C[id == %d] within 10 sec "
+                   "select s1.k as k, s1.price as p1, s2[last].price as p2, s3.ts as t3 insert into Seq%d;"
+                   % (repr(q / 32.0), q % 50, (q + 1) % 50, q))
+    seq.append(" end;")
+    agg = ["from A[price > %s] select k, sum(price) as total, count() as n "
+           "group by k having total > 1.0 insert into Agg%d;" % (repr((q - 32) / 32.0), q)
+           for q in range(32, 64)]
+    return ev + "".join(seq) + "".join(agg)
+
+
+CONFIG5_OUTPUTS = ["Seq%d" % q for q in range(32)] + ["Agg%d" % q for q in range(32, 64)]
+
+
+def config5_streams(price):
+    """Stream handle (0 = A, 1 = B, 2 = C) of each event for config 5: a
+    function of the generated price (numpy or torch), as the tests do."""
+    return (price * 1000).astype(np.int64) % 3 if isinstance(price, np.ndarray) else \
+        ((price * 1000).long() % 3)
+
+
 def splitmix64(x: np.ndarray) -> np.ndarray:
     with np.errstate(over="ignore"):
         z = x + np.uint64(GOLDEN)

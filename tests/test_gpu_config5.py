@@ -79,3 +79,30 @@ def test_config5_64_queries_two_batches():
         else:
             agg_rows += len(got[o])
     assert seq_rows > 20 and agg_rows > 1000, (seq_rows, agg_rows)
+
+
+def config5_exact_plan():
+    return workload.config5_plan()
+
+
+def test_config5_exact_predicates():
+    plan = config5_exact_plan()
+    # few keys, many events per key: strictly contiguous A, B+, C runs with
+    # id == q % 50 complete now and then; the aggregates emit on most A's
+    w = three_streams(24000, 4)
+    want = oracle_run(plan, events(w))
+    outs = ["Seq%d" % q for q in range(32)] + ["Agg%d" % q for q in range(32, 64)]
+    rt = fs.SiddhiAppRuntime(plan, key_capacity=64)
+    for o in outs:
+        rt.add_callback(o)
+    n = len(w["ts"])
+    for s, e in ((0, n // 3), (n // 3, n)):
+        rt.send("A", w["ts"][s:e], [w["k"][s:e], w["ts"][s:e], w["id"][s:e], w["price"][s:e]],
+                streams=w["stream"][s:e])
+        rt.flush()
+    got = {o: engine_rows(rt.collect(o)) for o in outs}
+    rt.shutdown()
+    for o in outs:
+        assert_same_rows(got[o], want.get(o, []), o)
+    assert sum(len(got[o]) for o in outs if o.startswith("Agg")) > 10000
+    assert sum(len(want.get(o, [])) for o in outs if o.startswith("Seq")) > 0
