@@ -145,7 +145,8 @@ __device__ __forceinline__ uint32_t eval_run(const TermList& tl, const VmArgs& v
 // kVm = false: filter and projection are TermList / direct copies (no interpreter).
 template <bool kVm>
 __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
-  __shared__ uint64_t R[kMaxRegs * kFilterThreads];
+  constexpr int kStageWords = 4096;   // plain-copy output stage (32 KiB)
+  __shared__ uint64_t R[kVm ? kMaxRegs * kFilterThreads : kStageWords];
   __shared__ uint32_t scratch[16];
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_prefix;
@@ -216,6 +217,41 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
   }
   __syncthreads();
   int64_t pos = (int64_t)s_prefix + off;
+  if constexpr (!kVm) {
+    // Plain-copy projection: stage the tile's selected rows in LDS column by
+    // column, then write each column's run [prefix, prefix +
+    // total) with consecutive lanes on consecutive rows — one contiguous
+    // store stream per column instead of one scattered store per row and
+    // column.  A tile selecting more rows than the stage holds, or one that
+    // would pass the output capacity, stores directly.
+    const int nc = a.out.ncols;
+    const uint32_t cap = (uint32_t)(kStageWords / (nc + 2));
+    const int64_t prefix = (int64_t)s_prefix;
+    if (total <= cap && prefix + (int64_t)total <= a.out.cap) {   // uniform
+      uint32_t slot = off;
+      while (sel) {
+        const int e = __ffs(sel) - 1;
+        sel &= sel - 1;
+        const int64_t row = row0 + e;
+        for (int c = 0; c < nc; ++c) {
+          const int col = a.out.src[c] - SRC_REC;
+          R[c * cap + slot] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], row);
+        }
+        R[nc * cap + slot] = (uint64_t)a.rows.ts[row];
+        R[(nc + 1) * cap + slot] = (uint64_t)(a.rows.seq0 + row);
+        ++slot;
+      }
+      __syncthreads();
+      for (int c = 0; c < nc; ++c)
+        for (uint32_t j = tid; j < total; j += kFilterThreads)
+          store_col(a.out.col[c], a.out.type[c], prefix + j, R[c * cap + j]);
+      for (uint32_t j = tid; j < total; j += kFilterThreads) {
+        a.out.ts[prefix + j] = (int64_t)R[nc * cap + j];
+        a.out.seq[prefix + j] = (int64_t)R[(nc + 1) * cap + j];
+      }
+      return;
+    }
+  }
   while (sel) {
     const int e = __ffs(sel) - 1;
     sel &= sel - 1;

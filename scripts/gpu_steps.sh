@@ -7,11 +7,11 @@
 mkdir -p gpurun_out
 for step in "$@"; do
   secs=${step%% *}; rest=${step#* }; name=${rest%% *}; cmd=${rest#* }
-  echo "[$(date +%T)] step $name: $cmd" | tee -a gpurun_out/steps.log
-  timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
+  echo "[$(date +%T)] step $name: $cmd" | tee -a gpurun_out/steps.txt
+  timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.txt" 2>&1
   rc=$?
-  echo "[$(date +%T)] step $name rc=$rc" | tee -a gpurun_out/steps.log
-  tail -3 "gpurun_out/$name.log"
+  echo "[$(date +%T)] step $name rc=$rc" | tee -a gpurun_out/steps.txt
+  tail -3 "gpurun_out/$name.txt"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 done
 exit 0
