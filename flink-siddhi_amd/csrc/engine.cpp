@@ -162,6 +162,7 @@ struct cep_app {
   DevBuf tile_state, ticket, err;
   DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
+  DevBuf str_hash;             // Java String.hashCode per dictionary id (dynamic routing)
   // host batches: two staging slots (pinned host arena + device arena); a
   // batch's H2D copy runs on the copy stream while the previous batch's
   // kernels run on the main stream
@@ -929,6 +930,13 @@ int cep_plan_schema(const char* plan, const char* stream_id, cep_attr* out, int 
 }
 
 cep_app* cep_create(const char* plan, const cep_options* opt, char* err, size_t errlen) {
+  return cep::create_app(plan, opt, nullptr, err, errlen);
+}
+
+}  // extern "C"
+
+cep_app* cep::create_app(const char* plan, const cep_options* opt, const std::vector<std::string>* dict_seed,
+                         char* err, size_t errlen) {
   if (!plan) {
     set_err(err, errlen, "plan is null");
     return nullptr;
@@ -943,7 +951,7 @@ cep_app* cep_create(const char* plan, const cep_options* opt, char* err, size_t 
   }
   if (a->opt.key_stride <= 0) a->opt.key_stride = 1;
   std::string m;
-  int rc = compile_app(plan, &a->app, &m);
+  int rc = compile_app(plan, &a->app, &m, dict_seed);
   if (rc) {
     set_err(err, errlen, m);
     delete a;
@@ -959,6 +967,8 @@ cep_app* cep_create(const char* plan, const cep_options* opt, char* err, size_t 
   set_err(err, errlen, "");
   return a;
 }
+
+extern "C" {
 
 void cep_destroy(cep_app* a) {
   if (!a) return;
@@ -1064,6 +1074,7 @@ void cep_destroy(cep_app* a) {
   dev_free(&a->route_dcount);
   dev_free(&a->ticket);
   dev_free(&a->err);
+  dev_free(&a->str_hash);
   if (a->stream) hipStreamSynchronize(a->stream);
   if (a->side) hipStreamSynchronize(a->side);
   for (auto& p : a->pats)
@@ -1906,6 +1917,108 @@ int cep_send_records(cep_app* a, const void* recs, int64_t n, int64_t events_rep
   rows.input = rt.pa.a_stream;
   a->batches++;
   return run_pattern(a, rt, rows, (const uint64_t*)recs, rt.pa.rec_words + 1);
+}
+
+int cep_plan_partition_keys(const char* plan, const char* stream_id, char* buf, size_t len) {
+  if (!plan || !stream_id || !buf || !len) return CEP_E_ARG;
+  CompiledApp app;
+  std::string m;
+  const int rc = compile_app(plan, &app, &m);
+  if (rc) return rc;
+  const int in = app.input_index(stream_id);
+  if (in < 0) return CEP_E_UNDEFINED_STREAM;
+  // SiddhiExecutionPlanner.parse (utils/SiddhiExecutionPlanner.java:76-140,
+  // retrievePartition :172-189): each query reading the stream names its
+  // group-by attributes; queries that name different non-empty lists are
+  // incompatible partitions.  Extension: the reference's planner rejects
+  // `partition with` blocks; here a partitioned query names its partition
+  // attribute of the stream.
+  const auto& attrs = app.inputs[in].attrs;
+  std::vector<int> keys;
+  for (auto& q : app.queries) {
+    std::vector<int> k;
+    if (q.in_stream == in) {
+      k = q.group_cols;
+      if (k.empty() && q.part_col >= 0) k.push_back(q.part_col);
+    } else if (q.nfa) {
+      if (in < (int)q.key_col_s.size() && q.key_col_s[in] >= 0) k.push_back(q.key_col_s[in]);
+    } else if (q.a_stream == in || q.b_stream == in) {
+      const int c = q.a_stream == in ? q.key_col_a : q.key_col_b;
+      if (c >= 0) k.push_back(c);
+    }
+    if (k.empty()) continue;
+    if (!keys.empty() && keys != k) {
+      std::snprintf(buf, len, "incompatible partitions on stream %s: [%s] vs [%s]", stream_id,
+                    attrs[keys[0]].name.c_str(), attrs[k[0]].name.c_str());
+      return CEP_E_PARSE;
+    }
+    keys = k;
+  }
+  std::string s;
+  for (int c : keys) {
+    if (!s.empty()) s += '\n';
+    s += attrs[c].name;
+  }
+  std::snprintf(buf, len, "%s", s.c_str());
+  return s.size() < len ? CEP_OK : CEP_E_CAPACITY;
+}
+
+int cep_partition_channels(cep_app* a, const cep_batch* b, const char* key_field, int nchan, int64_t seq0,
+                           int32_t* chan_dev, int64_t* keys_dev) {
+  if (!a || !b || nchan <= 0 || !chan_dev || !b->on_device || b->stream) return CEP_E_ARG;
+  if (b->input < 0 || b->input >= (int)a->app.inputs.size()) return fail(a, CEP_E_UNDEFINED_STREAM, "undefined input handle");
+  const StreamSchema& sd = a->app.inputs[b->input];
+  RouteKeyArgs ra{};
+  ra.n = b->n;
+  ra.nchan = nchan;
+  ra.seq0 = seq0;
+  ra.keys = keys_dev;
+  ra.chan = chan_dev;
+  if (key_field && *key_field) {
+    int c = -1;
+    for (size_t i = 0; i < sd.attrs.size(); ++i)
+      if (sd.attrs[i].name == key_field) c = (int)i;
+    if (c >= b->ncols) return fail(a, CEP_E_ARG, "batch has fewer columns than the stream definition");
+    if (c < 0) {
+      // AddRouteOperator.java:84-91: a key the stream lacks sums no field -> key 0
+      hipMemsetAsync(chan_dev, 0, (size_t)b->n * 4, a->stream);
+      if (keys_dev) hipMemsetAsync(keys_dev, 0, (size_t)b->n * 8, a->stream);
+      return hipGetLastError() == hipSuccess ? CEP_OK : fail(a, CEP_E_DEVICE, "memset failed");
+    }
+    ra.col = b->cols[c];
+    ra.type = sd.attrs[c].type;
+    if (ra.type == T_STRING) {
+      // String.hashCode over UTF-16 code units of each dictionary entry
+      std::vector<int32_t> h(a->dict.size());
+      for (size_t i = 0; i < a->dict.size(); ++i) {
+        const std::string& u = a->dict[i];
+        uint32_t x = 0;
+        for (size_t j = 0; j < u.size();) {
+          uint32_t cp = (uint8_t)u[j];
+          int extra = cp >= 0xf0 ? 3 : cp >= 0xe0 ? 2 : cp >= 0xc0 ? 1 : 0;
+          cp = extra == 3 ? (cp & 7) : extra == 2 ? (cp & 15) : extra == 1 ? (cp & 31) : cp;
+          for (int k = 1; k <= extra && j + k < u.size(); ++k) cp = (cp << 6) | ((uint8_t)u[j + k] & 63);
+          j += 1 + extra;
+          if (cp >= 0x10000) {   // surrogate pair
+            cp -= 0x10000;
+            x = x * 31u + (0xd800u + (cp >> 10));
+            x = x * 31u + (0xdc00u + (cp & 0x3ff));
+          } else {
+            x = x * 31u + cp;
+          }
+        }
+        h[i] = (int32_t)x;
+      }
+      if (!dev_ensure(&a->str_hash, std::max<size_t>(h.size(), 1) * 4, a->stream, false))
+        return fail(a, CEP_E_DEVICE, "out of device memory");
+      if (!h.empty()) hipMemcpyAsync(a->str_hash.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, a->stream);
+      hipStreamSynchronize(a->stream);
+      ra.str_hash = (const int32_t*)a->str_hash.p;
+      ra.nstr = (int32_t)h.size();
+    }
+  }
+  launch_route_keys(ra, a->stream);
+  return hipGetLastError() == hipSuccess ? CEP_OK : fail(a, CEP_E_DEVICE, "route key kernel failed");
 }
 
 int cep_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys, int64_t rate, int64_t t0,

@@ -1219,10 +1219,13 @@ void compile_single(CompiledApp* app, QueryAst& q) {
     bind_expr(g, c, app);
     CodeGen cg(app, raw);
     out.group_progs.push_back(cg.compile(g));
+    out.group_cols.push_back(g->col);
   }
   bool agg = !out.aggs.empty();
-  if (!agg && !q.group_by.empty())
-    fail(CEP_E_UNSUPPORTED, "group by without aggregates");
+  // group by without aggregates: Siddhi's selector evaluates each event's
+  // projection as it comes (no group state), so it is a plain projection; the
+  // attributes still name the plan's routing keys (cep_plan_partition_keys)
+  if (!agg) out.group_progs.clear();
   if (agg) {
     out.kind = Q_AGG;
     if (q.group_by.size() > 1)
@@ -1543,9 +1546,28 @@ void compile_pattern(CompiledApp* app, QueryAst& q) {
 
 }  // namespace
 
-int compile_app(const std::string& text, CompiledApp* out, std::string* err) {
+std::vector<int> read_inputs(const CompiledApp& app) {
+  std::vector<char> used(app.inputs.size(), 0);
+  auto mark = [&](int s) {
+    if (s >= 0 && s < (int)used.size()) used[s] = 1;
+  };
+  for (auto& q : app.queries) {
+    mark(q.in_stream);
+    mark(q.a_stream);
+    mark(q.b_stream);
+    for (auto& st : q.nstates) mark(st.stream);
+  }
+  std::vector<int> out;
+  for (size_t i = 0; i < used.size(); ++i)
+    if (used[i]) out.push_back((int)i);
+  return out;
+}
+
+int compile_app(const std::string& text, CompiledApp* out, std::string* err,
+                const std::vector<std::string>* dict_seed) {
   try {
     CompiledApp app;
+    if (dict_seed) app.strings = *dict_seed;
     std::vector<QueryAst> qs;
     Parser(text).parse(&app.inputs, &qs);
     for (auto& q : qs) {

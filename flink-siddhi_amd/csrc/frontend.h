@@ -62,6 +62,7 @@ struct Query {
   int key_col = -1;              // partition / group key column (-1: none)
   int part_col = -1;             // `partition with` column (-1: none)
   std::vector<Prog> group_progs; // group-by expressions (host path when not a column)
+  std::vector<int> group_cols;   // group-by attribute columns (routing keys)
   std::vector<AggSpec> aggs;
 
   // ---- 2-state pattern `[every] s1=A[f] -> s2=B[g] [within W]`
@@ -118,8 +119,24 @@ struct CompiledApp {
 };
 
 // Status codes mirror include/cep.h.
-int compile_app(const std::string& text, CompiledApp* out, std::string* err);
+// dict_seed: strings that take dictionary ids 0..n-1 before the plan's own
+// literals (plans of one operator share their ids, operator.cpp).
+int compile_app(const std::string& text, CompiledApp* out, std::string* err,
+                const std::vector<std::string>* dict_seed = nullptr);
+
+}  // namespace cep
+
+struct cep_app;
+struct cep_options;
+namespace cep {
+// cep_create with a dictionary seed (engine.cpp).
+cep_app* create_app(const char* plan, const cep_options* opt, const std::vector<std::string>* dict_seed,
+                    char* err, size_t errlen);
 
 const char* type_name(int t);
+
+// Input streams some query reads (InputStream.getUniqueStreamIds over the
+// plan's queries), in definition order.
+std::vector<int> read_inputs(const CompiledApp& app);
 
 }  // namespace cep

@@ -285,10 +285,24 @@ struct KeyMapArgs {
   unsigned int* err;
 };
 
+// Dynamic-path routing key per row (keymap.hip).
+struct RouteKeyArgs {
+  const void* col;             // key field column (nullptr: no group-by key -> random channel)
+  int32_t type;
+  int64_t n;
+  const int32_t* str_hash;     // STRING: Java String.hashCode() per dictionary id
+  int32_t nstr;
+  int32_t nchan;
+  int64_t seq0;                // arrival number of row 0 (random channel draw)
+  int64_t* keys;               // out: partition key (-1: none), or nullptr
+  int32_t* chan;               // out: channel
+};
+
 // --------------------------------------------------------------- launchers --
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_keymap(const KeyMapArgs& a, hipStream_t s);
+void launch_route_keys(const RouteKeyArgs& a, hipStream_t s);
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

@@ -111,7 +111,60 @@ __global__ void k_keymap(KeyMapArgs a) {
   if (row) a.out[i] = (int32_t)id;
 }
 
+// AddRouteOperator's partition key of each row (router/AddRouteOperator.java:
+// 83-92): |hashCode(field)| with Java's hashCode per attribute type, then
+// HashPartitioner's channel key % n (router/HashPartitioner.java:24-26); no
+// key field (-1) goes to a pseudo-random channel (DynamicPartitioner.java:
+// 53-55 draws java.util.Random; here a hash of the row's arrival number).
+__global__ void k_route_keys(RouteKeyArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  int64_t key = -1;
+  if (a.col) {
+    int32_t h = 0;
+    switch (a.type) {
+      case T_INT: h = ((const int32_t*)a.col)[i]; break;
+      case T_LONG: {
+        const uint64_t v = (uint64_t)((const int64_t*)a.col)[i];
+        h = (int32_t)(uint32_t)(v ^ (v >> 32));
+        break;
+      }
+      case T_FLOAT: {
+        const float f = ((const float*)a.col)[i];
+        h = f != f ? 0x7fc00000 : (int32_t)__float_as_uint(f);
+        break;
+      }
+      case T_DOUBLE: {
+        const double d = ((const double*)a.col)[i];
+        const uint64_t v = d != d ? 0x7ff8000000000000ull : (uint64_t)__double_as_longlong(d);
+        h = (int32_t)(uint32_t)(v ^ (v >> 32));
+        break;
+      }
+      case T_BOOL: h = ((const uint8_t*)a.col)[i] ? 1231 : 1237; break;
+      default: {   // STRING: dictionary id -> String.hashCode() of the entry
+        const int32_t id = ((const int32_t*)a.col)[i];
+        h = (id >= 0 && id < a.nstr) ? a.str_hash[id] : 0;
+      }
+    }
+    key = h < 0 ? -(int64_t)h : (int64_t)h;
+  }
+  if (a.keys) a.keys[i] = key;
+  int32_t ch;
+  if (key >= 0) {
+    ch = (int32_t)(key % a.nchan);
+  } else {
+    const uint64_t r = mix64((uint64_t)(a.seq0 + i));
+    ch = (int32_t)(r % (uint64_t)a.nchan);
+  }
+  a.chan[i] = ch;
+}
+
 }  // namespace
+
+void launch_route_keys(const RouteKeyArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  hipLaunchKernelGGL(k_route_keys, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+}
 
 void launch_keymap(const KeyMapArgs& a, hipStream_t s) {
   if (a.n <= 0) return;

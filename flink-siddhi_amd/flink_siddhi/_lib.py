@@ -157,6 +157,24 @@ SIGNATURES = {
     "cep_route_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
                                   C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "cep_send_records": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
+    "cep_operator_create": (C.c_void_p, [C.POINTER(cep_options), C.c_char_p, C.c_size_t]),
+    "cep_operator_destroy": (None, [C.c_void_p]),
+    "cep_operator_add_plan": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
+    "cep_operator_update_plan": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
+    "cep_operator_remove_plan": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "cep_operator_enable": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
+    "cep_operator_plan": (C.c_void_p, [C.c_void_p, C.c_char_p]),
+    "cep_operator_send": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(cep_batch),
+                                    C.POINTER(C.c_int)]),
+    "cep_operator_flush": (C.c_int, [C.c_void_p]),
+    "cep_operator_intern": (C.c_int32, [C.c_void_p, C.c_char_p]),
+    "cep_operator_lookup": (C.c_char_p, [C.c_void_p, C.c_int32]),
+    "cep_operator_plan_ids": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "cep_operator_last_error": (C.c_char_p, [C.c_void_p]),
+    "cep_plan_input_streams": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "cep_plan_partition_keys": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "cep_partition_channels": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_char_p, C.c_int,
+                                         C.c_int64, C.c_void_p, C.c_void_p]),
     "cep_generate": (C.c_int, [C.c_int64, C.c_int64, C.c_uint64, C.c_int64,
                                C.c_int64, C.c_int64, C.c_int, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -74,14 +74,27 @@ class SiddhiAppRuntime:
                 code = L.CEP_E_UNSUPPORTED
             L.raise_for(code, msg)
         self._h = C.c_void_p(h)
+        self._owned = True
         self._callbacks: Dict[str, object] = {}
         self._collected: Dict[str, List[OutputRows]] = {}
 
+    @classmethod
+    def _borrow(cls, handle: int, options) -> "SiddhiAppRuntime":
+        """A view of a runtime owned elsewhere (a plan of an operator.SiddhiOperator)."""
+        r = cls.__new__(cls)
+        r._lib = L.lib()
+        r.options = options
+        r._h = C.c_void_p(handle)
+        r._owned = False
+        r._callbacks = {}
+        r._collected = {}
+        return r
+
     # -- lifecycle -----------------------------------------------------------
     def shutdown(self):
-        if self._h:
+        if self._h and self._owned:
             self._lib.cep_destroy(self._h)
-            self._h = None
+        self._h = None
 
     def __del__(self):
         try:
@@ -273,6 +286,36 @@ class SiddhiAppRuntime:
                                               C.c_void_p(out.data_ptr()), out.shape[0], counts))
         self._signal_consumer(ts)
         return out, [int(c) for c in counts]
+
+    def partition_channels(self, stream_id: str, ts, cols: Sequence, key_field: Optional[str],
+                           nchan: int, seq0: int = 0, keys: bool = False):
+        """Dynamic-path routing of a device batch (AddRouteOperator.java:83-92 ->
+        DynamicPartitioner.java:43-60 -> HashPartitioner.java:24-26): the
+        channel of each row, |Java hashCode(key_field)| % nchan, as an int32
+        device tensor (and the int64 partition keys with keys=True).  No
+        key_field: key -1 and a pseudo-random channel."""
+        import torch
+        h = self.input_handle(stream_id)
+        defs = self.stream_definition(stream_id)
+        if not _is_device(ts):
+            raise ValueError("partition_channels() takes device-resident columns")
+        keep = []
+        ptrs = (C.c_void_p * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            p, k = _ptr(c, np.dtype(L.NUMPY_DTYPES[defs[i][1]]), True)
+            ptrs[i] = p
+            keep.append(k)
+        n = _len(ts)
+        chan = torch.empty(max(n, 1), dtype=torch.int32, device=ts.device)
+        kt = torch.empty(max(n, 1), dtype=torch.int64, device=ts.device) if keys else None
+        b = L.cep_batch(n=n, ts=C.c_void_p(ts.data_ptr()), stream=None, input=h, ncols=len(cols),
+                        cols=ptrs, on_device=1)
+        self._wait_producer(ts)
+        self._check(self._lib.cep_partition_channels(
+            self._h, C.byref(b), key_field.encode() if key_field else None, int(nchan), int(seq0),
+            C.c_void_p(chan.data_ptr()), C.c_void_p(kt.data_ptr()) if keys else None))
+        self._signal_consumer(ts)
+        return (chan[:n], kt[:n]) if keys else chan[:n]
 
     def send_records(self, recs, n: int, events_represented: int = 0):
         """Owner side: feed received shuffle records (source-rank order)."""

@@ -265,6 +265,53 @@ int cep_route_batch(cep_app* app, const cep_batch* batch, int world,
 int cep_send_records(cep_app* app, const void* recs, int64_t n,
                      int64_t events_represented);
 
+/* ---- dynamic plans (control events) ---------------------------------------
+ * One operator hosting many plans, as AbstractSiddhiOperator keeps one
+ * QueryRuntimeHandler per execution plan id (operator/AbstractSiddhiOperator.java:
+ * 114-176) and changes the set on control events (onEventReceived, :400-467;
+ * control/MetadataControlEvent.java, control/OperationControlEvent.java).
+ * Plans are independent runtimes: changing one leaves the others' state. */
+typedef struct cep_operator cep_operator;
+cep_operator* cep_operator_create(const cep_options* opt, char* err, size_t errlen);
+void cep_operator_destroy(cep_operator* op);
+/* MetadataControlEvent: added / updated / deleted execution plans.  Update
+ * replaces the plan's runtime (its state restarts, as the reference shuts
+ * the old handler down); delete of an unknown id is ignored. */
+int cep_operator_add_plan(cep_operator* op, const char* plan_id, const char* plan);
+int cep_operator_update_plan(cep_operator* op, const char* plan_id, const char* plan);
+int cep_operator_remove_plan(cep_operator* op, const char* plan_id);
+/* OperationControlEvent ENABLE_QUERY / DISABLE_QUERY (query id = plan id). */
+int cep_operator_enable(cep_operator* op, const char* plan_id, int enabled);
+/* The plan's runtime (callbacks, stats, snapshot), or NULL. */
+cep_app* cep_operator_plan(cep_operator* op, const char* plan_id);
+/* A single-stream batch (batch->stream == NULL) of stream_id to every enabled
+ * plan that reads it (router/AddRouteOperator.java:65-96); *plans_sent = fan-out. */
+int cep_operator_send(cep_operator* op, const char* stream_id, const cep_batch* batch, int* plans_sent);
+int cep_operator_flush(cep_operator* op);
+/* Shared string dictionary of the operator's plans (STRING columns sent with
+ * cep_operator_send carry these ids; a plan's output ids are the same). */
+int32_t cep_operator_intern(cep_operator* op, const char* s);
+const char* cep_operator_lookup(cep_operator* op, int32_t id);
+/* Plan ids, newline separated. */
+int cep_operator_plan_ids(cep_operator* op, char* buf, size_t len);
+const char* cep_operator_last_error(cep_operator* op);
+
+/* The input streams the plan's queries read (InputStream.getUniqueStreamIds
+ * over its queries; the router's inputStreamToExecutionPlans,
+ * router/AddRouteOperator.java:159-175), newline separated. */
+int cep_plan_input_streams(const char* plan, char* buf, size_t len);
+/* The plan's partition keys for stream_id: its queries' group-by attributes
+ * (utils/SiddhiExecutionPlanner.java:76-140), newline separated. */
+int cep_plan_partition_keys(const char* plan, const char* stream_id, char* buf, size_t len);
+/* Dynamic-path routing of a device batch (router/AddRouteOperator.java:83-92,
+ * router/DynamicPartitioner.java:43-60, router/HashPartitioner.java:24-26):
+ * key = |Java hashCode(key_field)| (Integer, Long, Float, Double, Boolean,
+ * String semantics), channel = key % nchan; key_field NULL / "" -> key -1 and
+ * a pseudo-random channel.  chan_dev / keys_dev (optional): device arrays of
+ * batch->n entries. */
+int cep_partition_channels(cep_app* app, const cep_batch* batch, const char* key_field, int nchan,
+                           int64_t seq0, int32_t* chan_dev, int64_t* keys_dev);
+
 /* Synthetic workload generator (bench / tests only — BASELINE.md §3):
  * r(i,j) = splitmix64(seed ^ (i*0x9E3779B97F4A7C15) ^ j); key = r(i,0) mod K;
  * stream = r(i,1)>>63 (0 = A, 1 = B, or 0 when single_stream); id = r(i,2) mod 50;
