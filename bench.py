@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--workload", choices=["pattern", "filter", "config5"], default="pattern")
     ap.add_argument("--events", type=int, default=0, help="events per step per GPU")
     ap.add_argument("--keys", type=int, default=1 << 20)
+    ap.add_argument("--keys-dist", choices=["uniform", "zipf"], default="uniform",
+                    help="zipf: the BASELINE.md §3 Zipf s=1.1 variant (workload.zipf_map remap)")
     ap.add_argument("--rate", type=int, default=400, help="events per ms")
     ap.add_argument("--chunk", type=int, default=1 << 25)
     ap.add_argument("--buckets-log2", type=int, default=0,
@@ -163,6 +165,24 @@ def pmc_traffic(kernel):
     return None
 
 
+_ZIPF = {}
+
+
+def remap_keys(args, k):
+    """--keys-dist zipf: key -> workload.zipf_map(keys)[key] (numpy or torch)."""
+    if args.keys_dist != "zipf":
+        return k
+    from flink_siddhi import workload
+    if "np" not in _ZIPF:
+        _ZIPF["np"] = workload.zipf_map(args.keys)
+    if isinstance(k, __import__("numpy").ndarray):
+        return _ZIPF["np"][k]
+    import torch
+    if "dev" not in _ZIPF:
+        _ZIPF["dev"] = torch.from_numpy(_ZIPF["np"]).to(k.device)
+    return _ZIPF["dev"][k.long()]
+
+
 # ---------------------------------------------------------------- pattern --
 def pattern_conds():
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -181,6 +201,7 @@ def pattern_parity(args, n, opts):
     CO, f, g = pattern_conds()
     rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, **dict(opts, profile=0))
     d = workload.generate_device(0, n, args.keys, rate=args.rate)
+    d["k"] = remap_keys(args, d["k"])
     rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
     _, seq, cols = rt.output_tensors("O", copy=False)
     got_m = int(seq.shape[0])
@@ -191,6 +212,7 @@ def pattern_parity(args, n, opts):
     torch.cuda.empty_cache()
     T, _, _ = host_cores()
     w = CO.generate(0, n, args.keys, rate=args.rate, threads=T)
+    w["k"] = remap_keys(args, w["k"])
     want_m, want_d, _ = CO.pattern_mt(w, args.keys, f, g, True, 10000, threads=T)
     kept = float(((w["stream"] == 0) & (w["price"] > 0.5)).sum() +
                  ((w["stream"] == 1) & (w["id"] % 7 == 0)).sum()) / n
@@ -274,6 +296,7 @@ def config5_parity(args, opts, n_check=20000):
     from helpers import engine_rows, oracle_run
     plan = workload.config5_plan()
     w = workload.generate(0, n_check, args.keys, rate=args.rate)
+    w["k"] = remap_keys(args, w["k"])
     w["stream"] = workload.config5_streams(w["price"]).astype(np.uint8)
     rt = fs.SiddhiAppRuntime(plan, **dict(opts, profile=0, ordered_output=1))
     for o in workload.CONFIG5_OUTPUTS:
@@ -355,6 +378,8 @@ def main():
         d = workload.generate_device(first, n, args.keys, rate=args.rate,
                                      single_stream=not pattern, device="cuda")
         d["first"] = first
+        if pattern or config5:
+            d["k"] = remap_keys(args, d["k"])
         if (pattern or config5) and world > 1 and not shuffle_mode:
             d["k"] = (d["k"] // world) * world + rank     # owned keys, same distribution
         if config5:
@@ -374,30 +399,56 @@ def main():
         for o in outs:
             rt.add_callback(o, lambda rows: delivered.__setitem__(0, delivered[0] + len(rows)), copy=False)
 
+    guard = [torch.cuda.Stream(), torch.cuda.Stream()] if shuffle_mode else None
+
+    def route(d, j):
+        recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
+                                world, seq0=d["first"], streams=d["stream"],
+                                out=bufs.get(("send", j)))
+        bufs[("send", j)] = recs
+        return recs, counts
+
+    def run_shuffle(blist):
+        # Software pipeline over steps, double-buffered send / receive: the
+        # route of step s+1 (engine route stream) and the record all-to-all of
+        # step s+1 (RCCL) run while the walk of step s runs on the engine stream.
+        from flink_siddhi import shuffle
+        if not blist:
+            return
+        cur = route(blist[0], 0)
+        for i in range(len(blist)):
+            j = i % 2
+            recs, counts = cur
+            torch.cuda.current_stream().wait_stream(guard[j])   # the walk that last read recv[j]
+            recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get(("recv", j)))
+            bufs[("recv", j)] = recv
+            rt.send_records(recv, m, n, signal=False)
+            rt.signal(guard[j])
+            if i + 1 < len(blist):
+                cur = route(blist[i + 1], 1 - j)
+        rt.flush()
+
     def step(d):
-        if shuffle_mode:
-            from flink_siddhi import shuffle
-            recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
-                                    world, seq0=d["first"], streams=d["stream"],
-                                    out=bufs.get("send"))
-            bufs["send"] = recs
-            recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get("recv"))
-            bufs["recv"] = recv
-            rt.send_records(recv, m, n)
-        elif pattern or config5:
+        if pattern or config5:
             rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
         else:
             rt.send("inputStream", d["ts"], [d["id"], d["name"], d["price"], d["ts"]])
         rt.flush()
 
-    for s in range(warm):
-        step(batches[s])
+    if shuffle_mode:
+        run_shuffle(batches[:warm])
+    else:
+        for s in range(warm):
+            step(batches[s])
     st0 = rt.stats()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(steps):
-        step(batches[warm + s])
+    if shuffle_mode:
+        run_shuffle(batches[warm:])
+    else:
+        for s in range(steps):
+            step(batches[warm + s])
     torch.cuda.synchronize()
     barrier(world)
     dt = time.perf_counter() - t0
@@ -481,7 +532,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64+int32+int64", "data": "synthetic (splitmix64 counter stream, BASELINE.md §3)",
             "config": ({"workload": "config3: keyed every A -> B within 10 sec, partition with k",
-                        "keys": args.keys, "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
+                        "keys": args.keys, "keys_dist": args.keys_dist if args.keys_dist == "uniform" else "zipf(s=1.1)",
+                        "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
                         "chunk_events": args.chunk, "parallelism": "key-sharded x%d" % world,
                         "ingest": (("%s all-to-all key shuffle" % ("rccl" if _coll_device() == "cuda"
                                                                     else "gloo host-staged"))
@@ -490,7 +542,8 @@ def main():
                        if pattern else
                        {"workload": "config5: 64 queries (32 every A, B+, C within 10 sec sequences with "
                                     "id == q%50, 32 group-by/having aggregations), 3 keyed streams",
-                        "keys": args.keys, "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
+                        "keys": args.keys, "keys_dist": args.keys_dist if args.keys_dist == "uniform" else "zipf(s=1.1)",
+                        "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
                         "parallelism": "key-sharded x%d (pre-partitioned)" % world}
                        if config5 else
                        {"workload": "config2: inputStream[price > 0.5 and id % 7 == 0] select *",

@@ -640,16 +640,21 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   auto sl_st = [&](int j, int w, uint64_t v) {
     *(uint64_t*)((char*)a.kslot + (kb + (uint32_t)(j * sw + w) * pb)) = v;
   };
-  uint32_t hdr = klane ? a.khdr[kidx] : 0u;
+  const uint32_t hdr = klane ? a.khdr[kidx] : 0u;
   // A pending list longer than the S inline slots keeps slots [S, n) in an
   // overflow run of the pending pool: header bit kHdrOvf set, kext = n |
   // run offset << 32 in this launch's read pool.  Runs are rewritten into the
   // write pool whenever the list is rebuilt (and moved there at kernel end
-  // otherwise): the host swaps the two pools per launch.
+  // otherwise): the host swaps the two pools per launch.  The run lives in
+  // one register: ovo = offset | kOvoWr (run in the write pool); the host
+  // keeps pool offsets below 2^31.
   const bool ovf0 = klane && (hdr & kHdrOvf);
-  uint64_t ext = ovf0 ? a.kext[kidx] : 0ull;
-  const uint64_t* ov = ovf0 ? a.pool_rd + (ext >> 32) * (uint64_t)p.slot_words : nullptr;
-  bool ov_wr = false;   // the overflow run lives in the write pool
+  const uint64_t ext0 = ovf0 ? a.kext[kidx] : 0ull;
+  uint32_t ovo = (uint32_t)(ext0 >> 32);
+  constexpr uint32_t kOvoWr = 0x80000000u;
+  auto ovp = [&]() -> const uint64_t* {
+    return ((ovo & kOvoWr) ? a.pool_wr : a.pool_rd) + (uint64_t)(ovo & ~kOvoWr) * (uint64_t)sw;
+  };
   // bucket-major offset table, loaded before the slot loads below (those
   // wait for hdr; these need not)
   const uint16_t* rlo = a.tile_off + (int64_t)bucket * ntiles;
@@ -681,7 +686,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   load_tile_off(rlo, lop);
   load_tile_off(rhi, ys);
 
-  int n = ovf0 ? (int)(uint32_t)ext : (int)(hdr & 0xffu);
+  int n = ovf0 ? (int)(uint32_t)ext0 : (int)(hdr & 0xffu);
   // Slots 0 / 1 (ts + captures) live in registers for the whole kernel: read
   // once here, rewritten by the commit of each window (named scalars: a
   // dynamically indexed array lands in scratch).  Word 1 of a slot (the A's
@@ -709,7 +714,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   uint32_t pcb = 0;
   auto slot_word = [&](int j, int w) -> uint64_t {
     if (j >= 2) {
-      if (j >= S) return ov[(int64_t)(j - S) * sw + w];
+      if (j >= S) return ovp()[(int64_t)(j - S) * sw + w];
       if (j - 2 < cn) return L.pcache[pcb + (uint32_t)((j - 2) * cw + (w == 0 ? 0 : w - 1))];
       return sl_ld(j, w);
     }
@@ -1140,14 +1145,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
                  cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
       }
       dirty |= nn != n;
-      if (nn > S) {
-        ov = nov;
-        ov_wr = true;
-        ext = (uint64_t)(uint32_t)nn | (noff << 32);
-      } else if (nn != n || n > S) {
-        ov = nullptr;
-        ov_wr = false;
-      }
+      if (nn > S) ovo = (uint32_t)noff | kOvoWr;
       n = nn;
     }
     CF_STAMP(wi * 8 + 6);
@@ -1194,22 +1192,23 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   }
   // ---- an overflow run still in the read pool moves to the write pool
   // (the read pool is the next launch's write pool)
-  if (klane && n > S && !ov_wr) {
+  if (klane && n > S && !(ovo & kOvoWr)) {
     const unsigned long long cnt = (unsigned long long)(n - S);
     const unsigned long long off = atomicAdd(a.pool_cursor, cnt);
     if (off + cnt > a.pool_cap) {
       set_err(a.err, ERR_POOL);
     } else {
       uint64_t* o = a.pool_wr + off * (uint64_t)sw;
-      for (int64_t i = 0; i < (int64_t)cnt * sw; ++i) o[i] = ov[i];
-      ext = (uint64_t)(uint32_t)n | (off << 32);
+      const uint64_t* src = ovp();
+      for (int64_t i = 0; i < (int64_t)cnt * sw; ++i) o[i] = src[i];
+      ovo = (uint32_t)off | kOvoWr;
       dirty = true;
     }
   }
   // ---- the key's header and register-resident slots 0 / 1, once
   if (klane && dirty) {
-    hdr = (hdr & ~(0xffu | kHdrOvf)) | (n > S ? ((uint32_t)S | kHdrOvf) : (uint32_t)n);
-    if (n > S) a.kext[kidx] = ext;
+    const uint32_t h1 = (a.khdr[kidx] & ~(0xffu | kHdrOvf)) | (n > S ? ((uint32_t)S | kHdrOvf) : (uint32_t)n);
+    if (n > S) a.kext[kidx] = (uint64_t)(uint32_t)n | ((uint64_t)(ovo & ~kOvoWr) << 32);
     if (n > 0) {
       sl_st(0, 0, t0r);
       if (c1) sl_st(0, 2, a0c0);
@@ -1220,7 +1219,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       if (c1) sl_st(1, 2, a1c0);
       if (c2) sl_st(1, 3, a1c1);
     }
-    a.khdr[kidx] = hdr;
+    a.khdr[kidx] = h1;
   }
 }
 

@@ -152,6 +152,10 @@ struct cep_app {
   hipEvent_t in_ready = nullptr;
   hipEvent_t ext_ready = nullptr;   // cep_stream_wait: producer stream of device inputs
   hipEvent_t out_ready = nullptr;   // cep_stream_signal: the engine's work so far
+  // Shuffle sender (cep_route_batch of device batches) runs on its own stream:
+  // routing step s+1 overlaps the walk of step s (it touches no walk state)
+  hipStream_t rstream = nullptr;
+  hipEvent_t r_ready = nullptr;
   bool enabled = true;
   std::string last_error;
   std::vector<std::string> dict;
@@ -300,7 +304,9 @@ int create_runtime(cep_app* a) {
       hipEventCreateWithFlags(&a->in_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&a->ext_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&a->out_ready, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&a->copy, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&a->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&a->rstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&a->r_ready, hipEventDisableTiming) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
@@ -1085,6 +1091,11 @@ void cep_destroy(cep_app* a) {
   if (a->in_ready) hipEventDestroy(a->in_ready);
   if (a->ext_ready) hipEventDestroy(a->ext_ready);
   if (a->out_ready) hipEventDestroy(a->out_ready);
+  if (a->r_ready) hipEventDestroy(a->r_ready);
+  if (a->rstream) {
+    hipStreamSynchronize(a->rstream);
+    hipStreamDestroy(a->rstream);
+  }
   if (a->side) hipStreamDestroy(a->side);
   if (a->copy) hipStreamDestroy(a->copy);
   if (a->stream) hipStreamDestroy(a->stream);
@@ -1460,7 +1471,8 @@ int cep_reset_output(cep_app* a) {
 int cep_stream_wait(cep_app* a, void* hip_stream) {
   if (!a) return CEP_E_ARG;
   if (hipEventRecord(a->ext_ready, (hipStream_t)hip_stream) != hipSuccess ||
-      hipStreamWaitEvent(a->stream, a->ext_ready, 0) != hipSuccess)
+      hipStreamWaitEvent(a->stream, a->ext_ready, 0) != hipSuccess ||
+      hipStreamWaitEvent(a->rstream, a->ext_ready, 0) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "cep_stream_wait: invalid stream");
   return CEP_OK;
 }
@@ -1468,7 +1480,9 @@ int cep_stream_wait(cep_app* a, void* hip_stream) {
 int cep_stream_signal(cep_app* a, void* hip_stream) {
   if (!a) return CEP_E_ARG;
   if (hipEventRecord(a->out_ready, a->stream) != hipSuccess ||
-      hipStreamWaitEvent((hipStream_t)hip_stream, a->out_ready, 0) != hipSuccess)
+      hipStreamWaitEvent((hipStream_t)hip_stream, a->out_ready, 0) != hipSuccess ||
+      hipEventRecord(a->r_ready, a->rstream) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)hip_stream, a->r_ready, 0) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "cep_stream_signal: invalid stream");
   return CEP_OK;
 }
@@ -1853,10 +1867,14 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   const int64_t tile_rows = fast ? kCfTile : kPartThreads * kPartItems;
   const int64_t ntiles = (b->n + tile_rows - 1) / tile_rows;
   const int wrw = rt.pa.rec_words + 1;
-  if (!dev_ensure(&a->route_arena, (size_t)ntiles * tile_rows * wrw * 8, a->stream, false) ||
-      !dev_ensure(&a->route_tcount, (size_t)ntiles * world * 4, a->stream, false) ||
-      !dev_ensure(&a->route_toffs, (size_t)ntiles * world * 4, a->stream, false) ||
-      !dev_ensure(&a->route_dcount, (size_t)world * 8, a->stream, false))
+  // device batches route on the route stream (ordered after the producer by
+  // cep_stream_wait), so the walk of the previous batch keeps running; host
+  // batches were staged on the engine stream and route there
+  hipStream_t rs = b->on_device ? a->rstream : a->stream;
+  if (!dev_ensure(&a->route_arena, (size_t)ntiles * tile_rows * wrw * 8, rs, false) ||
+      !dev_ensure(&a->route_tcount, (size_t)ntiles * world * 4, rs, false) ||
+      !dev_ensure(&a->route_toffs, (size_t)ntiles * world * 4, rs, false) ||
+      !dev_ensure(&a->route_dcount, (size_t)world * 8, rs, false))
     return fail(a, CEP_E_DEVICE, "out of device memory (route arena)");
   RouteArgs ra{};
   ra.rows = rows;
@@ -1870,7 +1888,7 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   ra.tcount = (uint32_t*)a->route_tcount.p;
   ra.err = (unsigned int*)a->err.p;
   {
-    LaunchTimer t(a, CEP_K_ROUTE);
+    LaunchTimer t(a, CEP_K_ROUTE, rs);
     if (fast) {
       CfRouteArgs ca{};
       ca.r = ra;
@@ -1879,18 +1897,20 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
       for (int i = 0; i < rt.pref.n; ++i)
         if (rows.cols.p[rt.pref.col[i]] == (const void*)rows.ts && rows.cols.t[rt.pref.col[i]] == T_LONG)
           ca.ts_slot = i;
-      launch_cf_route(ca, ntiles, a->stream);
+      launch_cf_route(ca, ntiles, rs);
       launch_route_collect(ra, ntiles, (uint32_t*)a->route_toffs.p,
-                           (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
+                           (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, rs);
     } else {
       launch_route(ra, ntiles, rt.part_vm, (uint32_t*)a->route_toffs.p,
-                   (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, a->stream);
+                   (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, rs);
     }
   }
-  if (slot >= 0) hipEventRecord(a->hs[slot].free, a->stream);
+  if (slot >= 0) hipEventRecord(a->hs[slot].free, rs);
+  // the per-owner counts: W words, read back on the route stream only (the
+  // all-to-all's split sizes are host values); the engine stream keeps going
   std::vector<unsigned long long> dc(world);
-  hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, a->stream);
-  if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "route failed");
+  hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, rs);
+  if (hipStreamSynchronize(rs) != hipSuccess) return fail(a, CEP_E_DEVICE, "route failed");
   int64_t total = 0;
   for (int d = 0; d < world; ++d) {
     counts_host[d] = (int64_t)dc[d];

@@ -317,14 +317,21 @@ class SiddhiAppRuntime:
         self._signal_consumer(ts)
         return (chan[:n], kt[:n]) if keys else chan[:n]
 
-    def send_records(self, recs, n: int, events_represented: int = 0):
-        """Owner side: feed received shuffle records (source-rank order)."""
+    def send_records(self, recs, n: int, events_represented: int = 0, signal: bool = True):
+        """Owner side: feed received shuffle records (source-rank order).
+        signal=False leaves torch's stream free to run ahead of the walk (the
+        caller keeps `recs` alive and unchanged, e.g. double-buffered, and
+        orders its reuse with signal())."""
         p = C.c_void_p(recs.data_ptr()) if n else None
         if n and getattr(recs, "is_cuda", False):
             self._wait_producer(recs)
         self._check(self._lib.cep_send_records(self._h, p, n, events_represented))
-        if n and getattr(recs, "is_cuda", False):
+        if n and signal and getattr(recs, "is_cuda", False):
             self._signal_consumer(recs)
+
+    def signal(self, stream):
+        """Make a torch stream wait for the engine's work queued so far."""
+        self._check(self._lib.cep_stream_signal(self._h, C.c_void_p(stream.cuda_stream)))
 
     def output_device(self, out_id: str):
         r = L.cep_rows()

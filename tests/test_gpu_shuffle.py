@@ -89,3 +89,64 @@ def test_fast_route_equals_general_route(world, monkeypatch):
     assert (ra[:, :4] == rb[:, :4]).all()
     is_b = ((ra[:, 0] >> 40) & 0xff) == 1
     assert (ra[is_b, 4] == rb[is_b, 4]).all()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_pipelined_route_overlaps_walk(world):
+    # the bench's multi-GPU step loop (bench.py run_shuffle): rank r's engine
+    # routes its slice of step s+1 on its route stream while the walk of step
+    # s runs on its engine stream; send / receive buffers double-buffered,
+    # reuse ordered by guard streams (send_records(signal=False) + signal)
+    steps, n_per, keys = 4, 40000, 2000
+    plan = workload.PATTERN_PLAN
+    rts = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=16384)
+           for r in range(world)]
+    for rt in rts:
+        rt.add_callback("O")
+    guard = [[torch.cuda.Stream(), torch.cuda.Stream()] for _ in range(world)]
+    bufs = {}
+    data = [[_dev(workload.generate((s * world + r) * n_per, n_per, keys, rate=1))
+             for r in range(world)] for s in range(steps)]
+
+    def route(s, j):
+        out = []
+        for r in range(world):
+            d = data[s][r]
+            recs, counts = rts[r].route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
+                                        seq0=(s * world + r) * n_per, streams=d["stream"],
+                                        out=bufs.get(("send", r, j)))
+            bufs[("send", r, j)] = recs
+            out.append((recs, counts))
+        return out
+
+    cur = route(0, 0)
+    for s in range(steps):
+        j = s % 2
+        offs = [np.concatenate([[0], np.cumsum(c)]) for _, c in cur]
+        for r in range(world):
+            torch.cuda.current_stream().wait_stream(guard[r][j])
+            m = sum(int(cur[src][1][r]) for src in range(world))
+            buf = bufs.get(("recv", r, j))
+            if buf is None or buf.shape[0] < m:
+                buf = torch.empty((max(m, 1), cur[0][0].shape[1]), dtype=torch.int64, device="cuda")
+                bufs[("recv", r, j)] = buf
+            o = 0
+            for src in range(world):   # the all-to-all, in source-rank order
+                a, b = offs[src][r], offs[src][r + 1]
+                buf[o:o + b - a].copy_(cur[src][0][a:b])
+                o += b - a
+            rts[r].send_records(buf, m, n_per, signal=False)
+            rts[r].signal(guard[r][j])
+        if s + 1 < steps:
+            cur = route(s + 1, 1 - j)
+    got = []
+    for rt in rts:
+        rt.flush()
+        got += engine_rows(rt.collect("O"))
+    got.sort(key=lambda t: t[1])
+    w = workload.generate(0, steps * world * n_per, keys, rate=1)
+    want = oracle_run(plan, workload_events(w)).get("O", [])
+    assert len(want) > 1000
+    assert_same_rows(got, want, "pipelined world=%d" % world)
+    for rt in rts:
+        rt.shutdown()
