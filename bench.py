@@ -370,7 +370,7 @@ def main():
     # RCCL all-to-all moves the records, each owner walks what it received;
     # "prepartitioned" — the input is already keyed upstream (Flink keyBy):
     # rank r draws only keys it owns, no exchange.
-    shuffle_mode = pattern and world > 1 and args.ingest == "shuffle"
+    shuffle_mode = (pattern or config5) and world > 1 and args.ingest == "shuffle"
     host_ingest = args.ingest in ("host", "host-pageable") and world == 1
     batches = []
     for s in range(warm + steps):
@@ -401,8 +401,13 @@ def main():
 
     guard = [torch.cuda.Stream(), torch.cuda.Stream()] if shuffle_mode else None
 
+    # pattern: k_cfroute with predicate push-down; config 5 (64 queries,
+    # sequences): whole rows (cep_route_rows)
+    route_fn = rt.route if pattern else rt.route_rows
+    send_fn = rt.send_records if pattern else rt.send_rows
+
     def route(d, j):
-        recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
+        recs, counts = route_fn("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
                                 world, seq0=d["first"], streams=d["stream"],
                                 out=bufs.get(("send", j)))
         bufs[("send", j)] = recs
@@ -422,7 +427,7 @@ def main():
             torch.cuda.current_stream().wait_stream(guard[j])   # the walk that last read recv[j]
             recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get(("recv", j)))
             bufs[("recv", j)] = recv
-            rt.send_records(recv, m, n, signal=False)
+            send_fn(recv, m, n, signal=False)
             rt.signal(guard[j])
             if i + 1 < len(blist):
                 cur = route(blist[i + 1], 1 - j)
@@ -544,7 +549,11 @@ def main():
                                     "id == q%50, 32 group-by/having aggregations), 3 keyed streams",
                         "keys": args.keys, "keys_dist": args.keys_dist if args.keys_dist == "uniform" else "zipf(s=1.1)",
                         "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
-                        "parallelism": "key-sharded x%d (pre-partitioned)" % world}
+                        "parallelism": "key-sharded x%d" % world,
+                        "ingest": (("%s all-to-all row shuffle" % ("rccl" if _coll_device() == "cuda"
+                                                                   else "gloo host-staged"))
+                                   if shuffle_mode else "pre-partitioned (keyed upstream)")
+                        if world > 1 else "local"}
                        if config5 else
                        {"workload": "config2: inputStream[price > 0.5 and id % 7 == 0] select *",
                         "events_per_step_per_gpu": n, "parallelism": "replicas x%d" % world}),

@@ -581,6 +581,7 @@ struct CfWalkLds {
 
 // One output row.  acap = the A's logical captures, b0 / b1 = the completing
 // B's physical words, bts / seq = its event ts and arrival number.
+template <bool KR>   // KR: sparse keys (output the partition value, key_rev)
 __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long pos, int64_t key,
                                         uint64_t acap0, uint64_t acap1, uint64_t b0, uint64_t b1,
                                         int64_t bts, int64_t seq) {
@@ -592,7 +593,7 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
     const int src = a.out.src[c];
     uint64_t v;
     if (src == SRC_KEY) {
-      v = a.key_rev ? a.key_rev[key] : (uint64_t)key;
+      v = KR ? a.key_rev[key] : (uint64_t)key;
     } else if (src >= SRC_CAP && src < SRC_REC) {
       v = (src - SRC_CAP) == 0 ? acap0 : acap1;
     } else {
@@ -607,7 +608,7 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
 
 }  // namespace
 
-template <int NW>
+template <int NW, bool KR>
 __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   // 2 workgroups per CU
   constexpr int NT = kCfWalkThreads, RW = 1 + NW, WIN = cf_window<NW>();
   constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
@@ -1061,7 +1062,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
           const int js = cfirst + j;
           const uint64_t x0 = j == 0 ? e00 : (j == 1 ? e10 : (c1 ? slot_word(js, 2) : 0ull));
           const uint64_t x1 = j == 0 ? e01 : (j == 1 ? e11 : (c2 ? slot_word(js, 3) : 0ull));
-          cf_emit(a, base + L.v[r0] + j, kv, x0, x1, b0, b1, bts, seq_base + (int64_t)L.sseq[fb]);
+          cf_emit<KR>(a, base + L.v[r0] + j, kv, x0, x1, b0, b1, bts, seq_base + (int64_t)L.sseq[fb]);
         }
       }
       const bool prune = W >= 0 && L.khasa[tid];
@@ -1076,16 +1077,17 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       // the write pool (rare: a key with more than S live partials)
       const uint32_t from = (lb == kNoB ? r0 : (uint32_t)lb);
       int cap = (lb == kNoB ? n : 0) + (int)(r1 - from);
-      uint64_t* nov = nullptr;
-      unsigned long long noff = 0;
+      // the new overflow run: pool_wr slot noff on (kNoOff: none / pool full)
+      constexpr uint32_t kNoOff = 0xffffffffu;
+      uint32_t noff = kNoOff;
       if (cap > S) {
         const unsigned long long cnt = (unsigned long long)(cap - S);
-        noff = atomicAdd(a.pool_cursor, cnt);
-        if (noff + cnt > a.pool_cap) {
+        const unsigned long long o = atomicAdd(a.pool_cursor, cnt);
+        if (o + cnt > a.pool_cap) {
           set_err(a.err, ERR_POOL);
           cap = S;
         } else {
-          nov = a.pool_wr + noff * (uint64_t)sw;
+          noff = (uint32_t)o;
         }
       }
       auto put_slot = [&](uint64_t ts, uint64_t x0, uint64_t x1) {
@@ -1098,11 +1100,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         a1c1 = (x1 & m1) | (a1c1 & ~m1);
         if (nn >= 2) CF_COUNT(4, 1);
         if (nn >= S) {   // overflow run
-          if (!nov) {   // the pool ran out (ERR_POOL set): keep the device safe
+          if (noff == kNoOff) {   // the pool ran out (ERR_POOL set): keep the device safe
             ++nn;
             return;
           }
-          uint64_t* o = nov + (int64_t)(nn - S) * sw;
+          uint64_t* o = a.pool_wr + ((uint64_t)noff + (uint64_t)(nn - S)) * (uint64_t)sw;
           o[0] = ts;
           if (c1) o[2] = x0;
           if (c2) o[3] = x1;
@@ -1145,7 +1147,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
                  cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
       }
       dirty |= nn != n;
-      if (nn > S) ovo = (uint32_t)noff | kOvoWr;
+      if (nn > S) ovo = noff | kOvoWr;
       n = nn;
     }
     CF_STAMP(wi * 8 + 6);
@@ -1168,7 +1170,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       const uint64_t x0 = cp0 < 0 ? (uint64_t)ats : (cp0 == 0 ? a0 : a1);
       const uint64_t x1 = cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1);
       const int64_t kl = ((int64_t)k << lg) | bucket;
-      cf_emit(a, base + L.v[q] + extra, kl * p.key_stride + p.key_offset, x0, x1,
+      cf_emit<KR>(a, base + L.v[q] + extra, kl * p.key_stride + p.key_offset, x0, x1,
               NW > 0 ? L.scap[0][nb] : 0ull, NW > 1 ? L.scap[NW > 1 ? 1 : 0][nb] : 0ull, bts,
               seq_base + (int64_t)L.sseq[nb]);
     }
@@ -1244,9 +1246,18 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
 
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
   switch (a.cf.nw) {
-    case 0: hipLaunchKernelGGL(k_cfwalk<0>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-    case 1: hipLaunchKernelGGL(k_cfwalk<1>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
-    default: hipLaunchKernelGGL(k_cfwalk<2>, dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a); break;
+    case 0:
+      if (a.key_rev) hipLaunchKernelGGL((k_cfwalk<0, true>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
+      else hipLaunchKernelGGL((k_cfwalk<0, false>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
+      break;
+    case 1:
+      if (a.key_rev) hipLaunchKernelGGL((k_cfwalk<1, true>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
+      else hipLaunchKernelGGL((k_cfwalk<1, false>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
+      break;
+    default:
+      if (a.key_rev) hipLaunchKernelGGL((k_cfwalk<2, true>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
+      else hipLaunchKernelGGL((k_cfwalk<2, false>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
+      break;
   }
 }
 

@@ -167,6 +167,8 @@ struct cep_app {
   DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   DevBuf str_hash;             // Java String.hashCode per dictionary id (dynamic routing)
+  HostBuf flush_words;         // cep_flush: error word + output cursors (pinned)
+  DevBuf rr_col[kMaxCols], rr_ts, rr_stream, rr_seq;   // cep_send_rows: unpacked rows
   // host batches: two staging slots (pinned host arena + device arena); a
   // batch's H2D copy runs on the copy stream while the previous batch's
   // kernels run on the main stream
@@ -735,7 +737,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
   if (rt.sparse) {
     // partition values -> dense slots (keymap.hip); the pattern then reads
     // the dense column in place of the key column
-    if (in_recs) return fail(a, CEP_E_UNSUPPORTED, "sparse_keys with the multi-GPU key shuffle");
+    if (in_recs || rows_all.seq) return fail(a, CEP_E_UNSUPPORTED, "sparse_keys with the multi-GPU key shuffle");
     const int kcol = rows_all.input == q.b_stream ? q.key_col_b : q.key_col_a;
     if (!dev_ensure(&rt.dense, (size_t)std::max<int64_t>(rows_all.n, 1) * 4 + 16, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (dense keys)");
@@ -770,7 +772,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
       return fail(a, CEP_E_ARG, "sparse_keys needs 16-byte aligned columns");
     return run_pattern_cf(a, rt, q, o, rows, cf);
   }
-  if (rt.cf && (in_recs || pref_aligned(rt.pref, rows_all))) {
+  if (rt.cf && !rows_all.seq && (in_recs || pref_aligned(rt.pref, rows_all))) {
     CfPlan cf;
     if (cf_plan(rt, rows_all, &cf, in_recs != nullptr))
       return run_pattern_cf(a, rt, q, o, rows_all, cf, in_recs, in_rec_words);
@@ -859,9 +861,16 @@ int send_device_rows(cep_app* a, const RowsArgs& rows) {
   return CEP_OK;
 }
 
+int device_error(cep_app* a, unsigned int e);
+
 int check_device_error(cep_app* a) {
   unsigned int e = 0;
   hipMemcpy(&e, a->err.p, sizeof(e), hipMemcpyDeviceToHost);
+  return device_error(a, e);
+}
+
+// Error flags read back -> status (the flags are cleared).
+int device_error(cep_app* a, unsigned int e) {
   if (!e) return CEP_OK;
   hipMemset(a->err.p, 0, 64);
   if (e & ERR_ORDER)   // root cause first: out-of-order input also defeats `within` pruning
@@ -1081,6 +1090,11 @@ void cep_destroy(cep_app* a) {
   dev_free(&a->ticket);
   dev_free(&a->err);
   dev_free(&a->str_hash);
+  host_free(&a->flush_words);
+  for (auto& d : a->rr_col) dev_free(&d);
+  dev_free(&a->rr_ts);
+  dev_free(&a->rr_stream);
+  dev_free(&a->rr_seq);
   if (a->stream) hipStreamSynchronize(a->stream);
   if (a->side) hipStreamSynchronize(a->side);
   for (auto& p : a->pats)
@@ -1363,22 +1377,30 @@ int cep_watermark(cep_app* a, int64_t mark) {
 
 int cep_flush(cep_app* a) {
   if (!a) return CEP_E_ARG;
+  // the error word and every output cursor in one pinned readback, one sync
+  const size_t no = a->outs.size();
+  if (!host_ensure(&a->flush_words, (no + 1) * 8)) return fail(a, CEP_E_DEVICE, "out of pinned host memory");
+  uint64_t* fw = (uint64_t*)a->flush_words.p;
+  fw[0] = 0;
+  hipMemcpyAsync(fw, a->err.p, 4, hipMemcpyDeviceToHost, a->stream);
+  for (size_t i = 0; i < no; ++i)
+    hipMemcpyAsync(fw + 1 + i, a->outs[i].count, 8, hipMemcpyDeviceToHost, a->stream);
   if (hipStreamSynchronize(a->stream) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "device failure during processing");
   harvest_timers(a);
-  int rc = check_device_error(a);
+  int rc = device_error(a, (unsigned int)fw[0]);
   // an output cursor past its capacity is a hard failure before any count
   // is used (the rows beyond cap were never written)
-  for (auto& o : a->outs) {
-    unsigned long long cnt = 0;
-    hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
+  for (size_t i = 0; i < no; ++i) {
+    auto& o = a->outs[i];
+    const unsigned long long cnt = fw[1 + i];
     if (cnt > (unsigned long long)o.cap && rc == CEP_OK)
       rc = fail(a, CEP_E_DEVICE, "output capacity exceeded on " + o.id + ": " + std::to_string(cnt) +
                                      " rows > " + std::to_string(o.cap));
   }
-  for (auto& o : a->outs) {
-    unsigned long long cnt = 0;
-    if (rc == CEP_OK) hipMemcpy(&cnt, o.count, sizeof(cnt), hipMemcpyDeviceToHost);
+  for (size_t i = 0; i < no; ++i) {
+    auto& o = a->outs[i];
+    const unsigned long long cnt = rc == CEP_OK ? fw[1 + i] : 0ull;
     a->matches_out += (int64_t)cnt;
     if (o.fn && cnt > 0 && rc == CEP_OK) {
       // one async D2H per column into pinned buffers, one sync
@@ -1428,7 +1450,7 @@ int cep_flush(cep_app* a) {
       rows.cols = ptrs.data();
       o.fn(o.user, &rows);
     }
-    hipMemset(o.count, 0, sizeof(unsigned long long));
+    hipMemsetAsync(o.count, 0, sizeof(unsigned long long), a->stream);
     o.bound = 0;
   }
   return rc;
@@ -1923,6 +1945,64 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   return CEP_OK;
 }
 
+// Row shuffle plan: per input handle the owner key column (-1: any owner,
+// the stream feeds stateless filters only; -2: no query reads it).  Every
+// query that keeps per-key state must key each stream it reads on one
+// attribute, the same for all such queries; the shipped streams must share
+// one column layout (the owner unpacks them into one multi-stream batch).
+static int row_route_plan(cep_app* a, int32_t (&kc)[8], int* layout) {
+  const CompiledApp& app = a->app;
+  const int ni = (int)app.inputs.size();
+  if (ni > 8) return fail(a, CEP_E_UNSUPPORTED, "row shuffle supports at most 8 input streams");
+  for (int i = 0; i < 8; ++i) kc[i] = -2;
+  auto need = [&](int s, int col) -> int {
+    if (s < 0 || s >= ni) return CEP_OK;
+    if (col < 0) return fail(a, CEP_E_UNSUPPORTED, "row shuffle: query state on stream " + app.inputs[s].id +
+                                                     " is not keyed (needs `partition with` or group by)");
+    if (kc[s] >= 0 && kc[s] != col)
+      return fail(a, CEP_E_UNSUPPORTED, "row shuffle: stream " + app.inputs[s].id + " is keyed on two attributes");
+    kc[s] = col;
+    return CEP_OK;
+  };
+  for (auto& q : app.queries) {
+    int rc = CEP_OK;
+    if (q.kind == Q_FILTER) {
+      if (q.in_stream >= 0 && kc[q.in_stream] == -2) kc[q.in_stream] = -1;
+      continue;
+    }
+    if (q.kind == Q_AGG) {
+      rc = need(q.in_stream, q.key_col);
+    } else if (q.nfa) {
+      for (auto& st : q.nstates) {
+        rc = need(st.stream, st.stream >= 0 && st.stream < (int)q.key_col_s.size() ? q.key_col_s[st.stream] : -1);
+        if (rc) break;
+      }
+    } else {
+      rc = need(q.a_stream, q.key_col_a);
+      if (!rc) rc = need(q.b_stream, q.key_col_b);
+    }
+    if (rc) return rc;
+  }
+  // a keyed stream also read by a filter keeps its key (filters are stateless)
+  *layout = -1;
+  for (int s = 0; s < ni; ++s) {
+    if (kc[s] == -2) continue;
+    if (*layout < 0) {
+      *layout = s;
+      continue;
+    }
+    const auto& x = app.inputs[*layout].attrs;
+    const auto& y = app.inputs[s].attrs;
+    bool same = x.size() == y.size();
+    for (size_t c = 0; same && c < x.size(); ++c) same = x[c].type == y[c].type;
+    if (!same)
+      return fail(a, CEP_E_UNSUPPORTED, "row shuffle: streams " + app.inputs[*layout].id + " and " +
+                                            app.inputs[s].id + " have different column types");
+  }
+  if (*layout < 0) return fail(a, CEP_E_UNSUPPORTED, "row shuffle: no query reads any input stream");
+  return CEP_OK;
+}
+
 int cep_send_records(cep_app* a, const void* recs, int64_t n, int64_t events_represented) {
   if (!a || (n > 0 && !recs) || n < 0) return CEP_E_ARG;
   if (!a->enabled) return CEP_OK;
@@ -1937,6 +2017,133 @@ int cep_send_records(cep_app* a, const void* recs, int64_t n, int64_t events_rep
   rows.input = rt.pa.a_stream;
   a->batches++;
   return run_pattern(a, rt, rows, (const uint64_t*)recs, rt.pa.rec_words + 1);
+}
+
+int cep_row_words(cep_app* a) {
+  if (!a) return -CEP_E_ARG;
+  int32_t kc[8];
+  int layout;
+  const int rc = row_route_plan(a, kc, &layout);
+  if (rc) return -rc;
+  return 3 + (int)a->app.inputs[layout].attrs.size();
+}
+
+int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out, int64_t rec_cap,
+                   int64_t* counts_host) {
+  if (!a || !b || !counts_host || world <= 0) return CEP_E_ARG;
+  if (world > kMaxWorld) return fail(a, CEP_E_ARG, "world exceeds " + std::to_string(kMaxWorld));
+  int32_t kc[8];
+  int layout;
+  int rc = row_route_plan(a, kc, &layout);
+  if (rc) return rc;
+  for (int d = 0; d < world; ++d) counts_host[d] = 0;
+  if (b->n == 0) return CEP_OK;
+  if (!rec_out || rec_cap < b->n)
+    return fail(a, CEP_E_ARG, "rec_out must hold at least n rows (" + std::to_string(b->n) + ")");
+  if (b->stream) {
+    // a multi-stream batch needs one layout for all its streams (batch_rows)
+  } else if (kc[b->input] != -2) {
+    const auto& x = a->app.inputs[layout].attrs;
+    const auto& y = a->app.inputs[b->input].attrs;
+    bool same = x.size() == y.size();
+    for (size_t c = 0; same && c < x.size(); ++c) same = x[c].type == y[c].type;
+    if (!same) return fail(a, CEP_E_UNSUPPORTED, "row shuffle: batch stream layout differs");
+  }
+  RowsArgs rows{};
+  int slot;
+  bool direct;
+  rc = batch_rows(a, b, &rows, &slot, &direct);
+  if (rc) return rc;
+  const int64_t tile_rows = kPartThreads * kPartItems;
+  const int64_t ntiles = (b->n + tile_rows - 1) / tile_rows;
+  const int wrw = 3 + rows.cols.n;
+  hipStream_t rs = b->on_device ? a->rstream : a->stream;
+  if (!dev_ensure(&a->route_arena, (size_t)ntiles * tile_rows * wrw * 8, rs, false) ||
+      !dev_ensure(&a->route_tcount, (size_t)ntiles * world * 4, rs, false) ||
+      !dev_ensure(&a->route_toffs, (size_t)ntiles * world * 4, rs, false) ||
+      !dev_ensure(&a->route_dcount, (size_t)world * 8, rs, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory (route arena)");
+  RowRouteArgs ra{};
+  ra.rows = rows;
+  ra.world = world;
+  ra.wrw = wrw;
+  ra.tile_rows = (int32_t)tile_rows;
+  ra.seq0 = seq0;
+  for (int i = 0; i < 8; ++i) ra.key_col_s[i] = kc[i];
+  ra.arena = (uint64_t*)a->route_arena.p;
+  ra.tcount = (uint32_t*)a->route_tcount.p;
+  ra.err = (unsigned int*)a->err.p;
+  {
+    LaunchTimer t(a, CEP_K_ROUTE, rs);
+    launch_route_rows(ra, ntiles, (uint32_t*)a->route_toffs.p, (unsigned long long*)a->route_dcount.p,
+                      (uint64_t*)rec_out, rs);
+  }
+  if (slot >= 0) hipEventRecord(a->hs[slot].free, rs);
+  std::vector<unsigned long long> dc(world);
+  hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, rs);
+  if (hipStreamSynchronize(rs) != hipSuccess) return fail(a, CEP_E_DEVICE, "row route failed");
+  int64_t total = 0;
+  for (int d = 0; d < world; ++d) {
+    counts_host[d] = (int64_t)dc[d];
+    total += (int64_t)dc[d];
+  }
+  if (total > b->n) return fail(a, CEP_E_DEVICE, "route produced more rows than the batch");
+  rc = check_device_error(a);
+  if (rc) return rc;
+  a->batches++;
+  return CEP_OK;
+}
+
+int cep_send_rows(cep_app* a, const void* recs, int64_t n, int64_t events_represented) {
+  if (!a || (n > 0 && !recs) || n < 0) return CEP_E_ARG;
+  if (!a->enabled) return CEP_OK;
+  int32_t kc[8];
+  int layout;
+  int rc = row_route_plan(a, kc, &layout);
+  if (rc) return rc;
+  a->events_in += events_represented;
+  if (n == 0) return CEP_OK;
+  const StreamSchema& sd = a->app.inputs[layout];
+  const int nc = (int)sd.attrs.size();
+  RowUnpackArgs ua{};
+  ua.recs = (const uint64_t*)recs;
+  ua.n = n;
+  ua.wrw = 3 + nc;
+  ua.ncols = nc;
+  bool ok = true;
+  for (int c = 0; c < nc && ok; ++c) {
+    ok = dev_ensure(&a->rr_col[c], (size_t)n * type_width(sd.attrs[c].type) + 16, a->stream, false);
+    ua.col[c] = a->rr_col[c].p;
+    ua.type[c] = sd.attrs[c].type;
+  }
+  ok = ok && dev_ensure(&a->rr_ts, (size_t)n * 8, a->stream, false) &&
+       dev_ensure(&a->rr_stream, (size_t)n + 16, a->stream, false) &&
+       dev_ensure(&a->rr_seq, (size_t)n * 8, a->stream, false);
+  if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (received rows)");
+  ua.ts = (int64_t*)a->rr_ts.p;
+  ua.stream = (uint8_t*)a->rr_stream.p;
+  ua.seq = (int64_t*)a->rr_seq.p;
+  {
+    LaunchTimer t(a, CEP_K_OTHER);
+    launch_unpack_rows(ua, a->stream);
+  }
+  RowsArgs rows{};
+  rows.cols.n = nc;
+  for (int c = 0; c < nc; ++c) {
+    rows.cols.p[c] = ua.col[c];
+    rows.cols.t[c] = sd.attrs[c].type;
+  }
+  rows.ts = ua.ts;
+  rows.stream = ua.stream;
+  rows.input = layout;
+  rows.row0 = 0;
+  rows.n = n;
+  rows.seq0 = 0;
+  rows.seq = ua.seq;
+  rows.prev_ts = INT64_MIN;
+  a->last_ts = INT64_MIN;
+  a->batches++;
+  return send_device_rows(a, rows);
 }
 
 int cep_plan_partition_keys(const char* plan, const char* stream_id, char* buf, size_t len) {

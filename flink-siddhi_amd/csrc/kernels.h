@@ -27,7 +27,13 @@ struct RowsArgs {
   int64_t n;               // rows in the slice
   int64_t seq0;            // arrival sequence number of batch row 0
   int64_t prev_ts;         // ts of the row before the slice (monotonicity check)
+  const int64_t* seq;      // per-row arrival numbers (rows received through the row
+                           // shuffle, cep_send_rows), or nullptr: seq0 + row
 };
+
+__device__ __forceinline__ int64_t row_seq(const RowsArgs& r, int64_t row) {
+  return r.seq ? r.seq[row] : r.seq0 + row;
+}
 
 struct VmArgs {
   const Ins* code;
@@ -154,6 +160,34 @@ struct PartArgs {
 
 // Multi-GPU key shuffle (sender side).
 constexpr int kMaxWorld = 64;
+
+// Row shuffle for multi-query apps (cep_route_rows): every row a query reads
+// is shipped whole as [stream, seq, ts, column words...] to owner key % world
+// (key_col_s[stream] >= 0), or round-robin by arrival number for streams only
+// stateless filters read (key_col_s = -1); key_col_s = -2: not shipped.
+struct RowRouteArgs {
+  RowsArgs rows;
+  int32_t world;
+  int32_t wrw;                 // 3 + columns
+  int32_t tile_rows;
+  int64_t seq0;                // global arrival number of batch row 0
+  int32_t key_col_s[8];
+  uint64_t* arena;             // [ntiles][tile_rows * wrw], owner-grouped per tile
+  uint32_t* tcount;            // [ntiles][world]
+  unsigned int* err;
+};
+
+struct RowUnpackArgs {
+  const uint64_t* recs;
+  int64_t n;
+  int32_t wrw;
+  int32_t ncols;
+  void* col[kMaxCols];
+  int32_t type[kMaxCols];
+  int64_t* ts;
+  uint8_t* stream;
+  int64_t* seq;
+};
 struct RouteArgs {
   RowsArgs rows;
   VmArgs vm;
@@ -309,6 +343,9 @@ void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
                   unsigned long long* dcount, uint64_t* out, hipStream_t s);
 void launch_route_collect(const RouteArgs& a, int64_t ntiles, uint32_t* toffs,
                           unsigned long long* dcount, uint64_t* out, hipStream_t s);
+void launch_route_rows(const RowRouteArgs& a, int64_t ntiles, uint32_t* toffs,
+                       unsigned long long* dcount, uint64_t* out, hipStream_t s);
+void launch_unpack_rows(const RowUnpackArgs& a, hipStream_t s);
 void launch_cf_route(const CfRouteArgs& a, int64_t ntiles, hipStream_t s);
 void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s);
 // event-time reorder (reorder.hip)

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
           R[c * cap + slot] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], row);
         }
         R[nc * cap + slot] = (uint64_t)a.rows.ts[row];
-        R[(nc + 1) * cap + slot] = (uint64_t)(a.rows.seq0 + row);
+        R[(nc + 1) * cap + slot] = (uint64_t)row_seq(a.rows, row);
         ++slot;
       }
       __syncthreads();
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
         store_col(a.out.col[c], a.out.type[c], pos, v);
       }
       a.out.ts[pos] = a.rows.ts[row];
-      a.out.seq[pos] = a.rows.seq0 + row;
+      a.out.seq[pos] = row_seq(a.rows, row);
     }
     ++pos;
   }
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
     seq_base = (int64_t)a.in_recs[a.rows.row0 * a.in_rec_words + 1];
   } else {
     ts_base = a.rows.ts[a.rows.row0];
-    seq_base = a.rows.seq0 + a.rows.row0;
+    seq_base = row_seq(a.rows, a.rows.row0);
   }
   if (tile == 0 && tid == 0 && a.chunk_base) {
     a.chunk_base[0] = ts_base;
@@ -590,7 +590,12 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       }
       if (dts > 0x7fffffffll || dts < -0x7fffffffll) set_err(a.err, ERR_ORDER);
       put(0, (uint64_t)(uint32_t)key[e] | ((uint64_t)role << 32) | ((uint64_t)(uint32_t)s << 40));
-      put(1, (uint64_t)(uint32_t)(r - a.rows.row0) | ((uint64_t)(uint32_t)(int32_t)dts << 32));
+      int64_t dseq = r - a.rows.row0;
+      if (a.rows.seq) {   // shuffled rows: global arrival numbers, increasing
+        dseq = a.rows.seq[r] - seq_base;
+        if (dseq < 0 || dseq > 0xffffffffll) set_err(a.err, ERR_ORDER);
+      }
+      put(1, (uint64_t)(uint32_t)dseq | ((uint64_t)(uint32_t)(int32_t)dts << 32));
       const bool isa = s == p.a_stream;
       if constexpr (kPf) {
         // at most kPfRec carried words (host-checked); slots are uniform
@@ -735,6 +740,98 @@ __global__ __launch_bounds__(kPartThreads) void k_route(RouteArgs a) {
       o[3 + c] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], r);
     }
   }
+}
+
+// Row shuffle for multi-query apps (sequences, aggregations, several
+// patterns): no predicate push-down (a sequence needs every row of its
+// streams for strict contiguity), whole rows shipped as
+// [stream, seq, ts, column words] grouped by owner in arrival order.
+__global__ __launch_bounds__(kPartThreads) void k_route_rows(RowRouteArgs a) {
+  __shared__ uint32_t scratch[16];
+  __shared__ uint32_t dbase[kMaxWorld + 1];
+  const int tid = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  constexpr int E = kPartItems;
+  const int64_t r0 = tile * (int64_t)a.tile_rows + (int64_t)tid * E;
+  const int64_t nvalid = a.rows.n - r0;
+  const int64_t row0 = a.rows.row0 + r0;
+  int dest[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    dest[e] = -1;
+    if (e >= nvalid) continue;
+    const int sid = a.rows.stream ? (int)a.rows.stream[row0 + e] : a.rows.input;
+    const int kc = sid < 8 ? a.key_col_s[sid] : -2;
+    if (kc == -2) continue;   // no query reads the stream
+    if (kc == -1) {           // read by stateless filters only: round-robin
+      dest[e] = (int)((uint64_t)(a.seq0 + (row0 + e - a.rows.row0)) % (uint64_t)a.world);
+      continue;
+    }
+    const int64_t key = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e);
+    if (key < 0 || key > 0xffffffffll) {
+      set_err(a.err, ERR_KEY_RANGE);
+      continue;
+    }
+    dest[e] = (int)(key % a.world);
+  }
+  uint32_t rank[E];
+  for (int d = 0; d < a.world; ++d) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) c += dest[e] == d ? 1u : 0u;
+    uint32_t total;
+    uint32_t off = block_excl_scan(c, scratch, &total);
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (dest[e] == d) rank[e] = off++;
+    if (tid == 0) {
+      dbase[d] = d == 0 ? 0u : dbase[d - 1] + a.tcount[tile * a.world + d - 1];
+      a.tcount[tile * a.world + d] = total;
+    }
+    lds_barrier();
+  }
+  const int wrw = a.wrw;
+  uint64_t* base = a.arena + tile * (int64_t)a.tile_rows * wrw;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (dest[e] < 0) continue;
+    const int64_t r = row0 + e;
+    uint64_t* o = base + (int64_t)(dbase[dest[e]] + rank[e]) * wrw;
+    o[0] = a.rows.stream ? (uint64_t)a.rows.stream[r] : (uint64_t)a.rows.input;
+    o[1] = (uint64_t)(a.seq0 + (r - a.rows.row0));
+    o[2] = (uint64_t)a.rows.ts[r];
+    for (int c = 0; c < a.rows.cols.n; ++c) o[3 + c] = load_col(a.rows.cols.p[c], a.rows.cols.t[c], r);
+  }
+}
+
+// Owner side of the row shuffle: received rows -> SoA columns + per-row
+// stream handle and global arrival number.
+__global__ __launch_bounds__(256) void k_unpack_rows(RowUnpackArgs a) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t* r = a.recs + i * a.wrw;
+    a.stream[i] = (uint8_t)r[0];
+    a.seq[i] = (int64_t)r[1];
+    a.ts[i] = (int64_t)r[2];
+    for (int c = 0; c < a.ncols; ++c) store_col(a.col[c], a.type[c], i, r[3 + c]);
+  }
+}
+
+void launch_route_rows(const RowRouteArgs& a, int64_t ntiles, uint32_t* toffs,
+                       unsigned long long* dcount, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_route_rows, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
+  RouteArgs ra{};
+  ra.world = a.world;
+  ra.wrw = a.wrw;
+  ra.tile_rows = a.tile_rows;
+  ra.arena = a.arena;
+  ra.tcount = a.tcount;
+  launch_route_collect(ra, ntiles, toffs, dcount, out, s);
+}
+
+void launch_unpack_rows(const RowUnpackArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  const int64_t blocks = (a.n + 255) / 256 < 8192 ? (a.n + 255) / 256 : 8192;
+  hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
 
 // Per owner: exclusive prefix of its segment sizes over tiles.

@@ -157,6 +157,10 @@ SIGNATURES = {
     "cep_route_batch": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
                                   C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
     "cep_send_records": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
+    "cep_row_words": (C.c_int, [C.c_void_p]),
+    "cep_route_rows": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
+                                 C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
+    "cep_send_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]),
     "cep_operator_create": (C.c_void_p, [C.POINTER(cep_options), C.c_char_p, C.c_size_t]),
     "cep_operator_destroy": (None, [C.c_void_p]),
     "cep_operator_add_plan": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),

@@ -317,6 +317,54 @@ class SiddhiAppRuntime:
         self._signal_consumer(ts)
         return (chan[:n], kt[:n]) if keys else chan[:n]
 
+    def row_words(self) -> int:
+        w = self._lib.cep_row_words(self._h)
+        if w < 0:
+            self._check(-w)
+        return w
+
+    def route_rows(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int,
+                   streams=None, out=None):
+        """Sender side of the row shuffle (multi-query apps, no push-down):
+        (rows, counts) — an int64 device tensor [n, row_words] grouped by
+        owner in arrival order, and the per-owner row counts."""
+        import torch
+        h = self.input_handle(stream_id)
+        defs = self.stream_definition(stream_id)
+        if not _is_device(ts):
+            raise ValueError("route_rows() takes device-resident columns")
+        keep = []
+        ptrs = (C.c_void_p * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            p, k = _ptr(c, np.dtype(L.NUMPY_DTYPES[defs[i][1]]), True)
+            ptrs[i] = p
+            keep.append(k)
+        sp = None
+        if streams is not None:
+            sp, k = _ptr(streams, np.dtype("uint8"), True)
+            keep.append(k)
+        n = _len(ts)
+        w = self.row_words()
+        if out is None or out.shape[0] < n:
+            out = torch.empty((max(n, 1), w), dtype=torch.int64, device=ts.device)
+        b = L.cep_batch(n=n, ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
+                        cols=ptrs, on_device=1)
+        counts = (C.c_int64 * world)()
+        self._wait_producer(ts)
+        self._check(self._lib.cep_route_rows(self._h, C.byref(b), world, seq0,
+                                             C.c_void_p(out.data_ptr()), out.shape[0], counts))
+        self._signal_consumer(ts)
+        return out, [int(c) for c in counts]
+
+    def send_rows(self, rows, n: int, events_represented: int = 0, signal: bool = True):
+        """Owner side of the row shuffle: received rows in source-rank order."""
+        p = C.c_void_p(rows.data_ptr()) if n else None
+        if n and getattr(rows, "is_cuda", False):
+            self._wait_producer(rows)
+        self._check(self._lib.cep_send_rows(self._h, p, n, events_represented))
+        if n and signal and getattr(rows, "is_cuda", False):
+            self._signal_consumer(rows)
+
     def send_records(self, recs, n: int, events_represented: int = 0, signal: bool = True):
         """Owner side: feed received shuffle records (source-rank order).
         signal=False leaves torch's stream free to run ahead of the walk (the

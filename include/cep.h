@@ -264,6 +264,21 @@ int cep_route_batch(cep_app* app, const cep_batch* batch, int world,
                     int64_t* counts_host);
 int cep_send_records(cep_app* app, const void* recs, int64_t n,
                      int64_t events_represented);
+/* Row shuffle for apps with several queries (sequences, aggregations, more
+ * than one pattern; BASELINE config 5 across GPUs).  No predicate push-down:
+ * a sequence needs every row of its streams (strict contiguity).  Every row
+ * some query reads is shipped whole as cep_row_words() int64 words
+ * [stream handle, global arrival number, ts, one word per column] to owner
+ * key % world, key = the stream's partition / group-by attribute (streams
+ * only stateless filters read go round-robin by arrival number).  Rows come
+ * out grouped by owner, in arrival order, like cep_route_batch; the owner
+ * feeds what it received, in source-rank order, to cep_send_rows.
+ * CEP_E_UNSUPPORTED when a stateful query is not keyed, or keys a stream on
+ * two attributes, or the shipped streams differ in column types. */
+int cep_row_words(cep_app* app);   /* < 0: -status */
+int cep_route_rows(cep_app* app, const cep_batch* batch, int world, int64_t seq0, void* rec_out,
+                   int64_t rec_cap, int64_t* counts_host);
+int cep_send_rows(cep_app* app, const void* recs, int64_t n, int64_t events_represented);
 
 /* ---- dynamic plans (control events) ---------------------------------------
  * One operator hosting many plans, as AbstractSiddhiOperator keeps one

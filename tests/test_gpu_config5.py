@@ -106,3 +106,64 @@ def test_config5_exact_predicates():
         assert_same_rows(got[o], want.get(o, []), o)
     assert sum(len(got[o]) for o in outs if o.startswith("Agg")) > 10000
     assert sum(len(want.get(o, [])) for o in outs if o.startswith("Seq")) > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_config5_row_shuffle_matches_oracle(world):
+    # config 5 across GPUs (simulated worlds on one GPU): each source slice is
+    # routed whole-row by cep_route_rows (no push-down: sequences need every
+    # row), owner r receives the slices' r-segments in source order and runs
+    # them through cep_send_rows on an engine owning keys k % world == r; the
+    # merged outputs equal the single-stream oracle
+    import torch
+    plan = config5_plan()
+    n, keys = 9000, 48
+    n -= n % (2 * world)
+    w = three_streams(n, keys)
+    want = oracle_run(plan, events(w))
+    sender = fs.SiddhiAppRuntime(plan, key_capacity=64)
+    words = sender.row_words()
+    assert words == 3 + 4
+    owners = [fs.SiddhiAppRuntime(plan, key_capacity=64, key_stride=world, key_offset=r)
+              for r in range(world)]
+    for o in owners:
+        for out in outputs():
+            o.add_callback(out)
+    m = n // (2 * world)
+    for step in range(2):   # two shuffle steps: state carries across them
+        segs = [[] for _ in range(world)]
+        for src in range(world):
+            # as bench.py: rank src holds global slice step * world + src
+            s = (step * world + src) * m
+            e = s + m
+            d = {c: torch.from_numpy(np.ascontiguousarray(w[c][s:e])).cuda()
+                 for c in ("k", "ts", "id", "price", "stream")}
+            rows, counts = sender.route_rows("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
+                                             world, seq0=int(s), streams=d["stream"])
+            off = np.concatenate([[0], np.cumsum(counts)])
+            for r in range(world):
+                segs[r].append(rows[off[r]:off[r + 1]].clone())
+        for r in range(world):
+            recv = torch.cat(segs[r], dim=0)
+            owners[r].send_rows(recv, recv.shape[0], 0)
+    got = {o: [] for o in outputs()}
+    for r in range(world):
+        owners[r].flush()
+        for o in outputs():
+            got[o] += engine_rows(owners[r].collect(o))
+    # merge the owners' outputs by arrival number (rows of one seq come from
+    # one owner, in emission order)
+    for o in outputs():
+        got[o].sort(key=lambda t: t[1])
+        assert_same_rows(got[o], want.get(o, []), "%s world=%d" % (o, world))
+    assert sum(len(v) for v in got.values()) > 1000
+    for rt in owners + [sender]:
+        rt.shutdown()
+
+
+def test_row_shuffle_rejects_unkeyed_state():
+    plan = EV3 + "from A select sum(price) as s insert into O;"
+    rt = fs.SiddhiAppRuntime(plan)
+    with pytest.raises(fs.UnsupportedPlanException, match="not keyed"):
+        rt.row_words()
+    rt.shutdown()
