@@ -163,14 +163,15 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
   __shared__ uint32_t scratch[NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) uint64_t stage[kStageRecs * RW];
-  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // P + 1 (dynamic)
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // NB + 1 (dynamic)
   const int tid = threadIdx.x;
   const int64_t tile = xcd_tile(blockIdx.x, a.ntiles);
   const PatternArgs& p = a.pat;
   const int lg = p.buckets_log2;
   const int P = 1 << lg;
+  const int NB = P + a.nhot;   // key buckets, then one bucket per hot key (hot.hip)
   CF_STAMP(0);
-  for (int i = tid; i <= P; i += NT) hist[i] = 0;
+  for (int i = tid; i <= NB; i += NT) hist[i] = 0;
 
   const int64_t ts_base = FR ? (int64_t)a.in_recs[a.rows.row0 * a.in_rec_words + 2] : a.rows.ts[a.rows.row0];
   if (tile == 0 && tid == 0) {
@@ -284,23 +285,30 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
       set_err(a.err, ERR_KEY_RANGE);
       continue;
     }
-    const uint32_t bucket = (uint32_t)(kfield & (P - 1));
+    uint32_t bucket = (uint32_t)(kfield & (P - 1));
     lkey[e] = (uint32_t)(kfield >> lg);
+    if (a.nhot) {
+      const uint32_t hs = a.hot_id[kfield];
+      if (hs != kNotHot) {   // hot key: its own bucket; the key field holds the slot
+        bucket = (uint32_t)P + hs;
+        lkey[e] = hs;
+      }
+    }
     const uint32_t rank = atomicAdd(&hist[bucket], 1u);
     packed[e] = (role << 25) | (bucket << 13) | rank;
   }
   lds_barrier();
   CF_STAMP(2);
   {
-    // exclusive scan of the P bucket counts (P <= 4096: <= 8 per thread)
+    // exclusive scan of the NB bucket counts (NB <= 4096: <= 8 per thread)
     constexpr int MAXPER = kCfMaxBuckets / NT;
-    const int per = (P + NT - 1) / NT;
+    const int per = (NB + NT - 1) / NT;
     uint32_t c[MAXPER];
     uint32_t sum = 0;
 #pragma unroll
     for (int i = 0; i < MAXPER; ++i) {
       const int idx = tid * per + i;
-      c[i] = (i < per && idx < P) ? hist[idx] : 0u;
+      c[i] = (i < per && idx < NB) ? hist[idx] : 0u;
       sum += c[i];
     }
     uint32_t total;
@@ -308,16 +316,16 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
 #pragma unroll
     for (int i = 0; i < MAXPER; ++i) {
       const int idx = tid * per + i;
-      if (i < per && idx < P) {
+      if (i < per && idx < NB) {
         hist[idx] = off;
         off += c[i];
       }
     }
-    if (tid == 0) hist[P] = total;
+    if (tid == 0) hist[NB] = total;
   }
   lds_barrier();
   CF_STAMP(3);
-  const uint32_t total = hist[P];
+  const uint32_t total = hist[NB];
   const bool staged = total <= (uint32_t)kStageRecs;   // uniform
   uint64_t* trecs = a.recs + tile * (int64_t)kCfTile * RW;
 #pragma unroll
@@ -343,7 +351,7 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
       if (NW > 1) g[2] = c1;
     }
   }
-  for (int i = tid; i <= P; i += NT) a.tile_off[(int64_t)i * a.ntiles + tile] = (uint16_t)hist[i];
+  for (int i = tid; i <= NB; i += NT) a.tile_off[(int64_t)i * a.ntiles + tile] = (uint16_t)hist[i];
   if (staged) {
     lds_barrier();
     CF_STAMP(4);
@@ -628,8 +636,10 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   CF_STAMP(0);
 
   // ---- key lane (tid < kpb): pending count + slots 0 / 1 in registers,
-  // loaded now so the state read overlaps the gather below
-  const bool klane = tid < kpb;
+  // loaded now so the state read overlaps the gather below.  A hot key's
+  // records were diverted to the hot path this launch: its state is not ours.
+  const bool klane = tid < kpb && !(a.hot_id && a.hot_id[((int64_t)tid << lg) | bucket] != kNotHot);
+  uint32_t kcnt = 0;   // the key's records this launch (hot-key candidates)
   const int64_t kidx = (int64_t)bucket * kpb + tid;
   // slot j word w of this key at byte kb + (j * sw + w) * pb of kslot: 32-bit
   // offsets from the kernel-argument base (the host checks the state fits
@@ -980,6 +990,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     if (klane) {
       r0 = L.kstart[tid];
       r1 = L.kstart[tid + 1];
+      kcnt += r1 - r0;
       const uint16_t fb = L.kfb[tid];
       if (r1 > r0 && fb != kNoB && n > 0) {
         const int64_t tb = ts_base + (int64_t)L.sts[fb];
@@ -1192,6 +1203,12 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
     lds_barrier();
   }
+  // ---- hot-key candidates: keys that made this bucket long (hot.hip)
+  if (klane && a.hot_thresh && kcnt > a.hot_thresh) {
+    const uint32_t i = atomicAdd(a.hot_ncand, 1u);
+    if (i < (uint32_t)kCfHotMax * 4)
+      a.hot_cand[i] = ((uint64_t)kcnt << 32) | (uint64_t)(uint32_t)(((int64_t)tid << lg) | bucket);
+  }
   // ---- an overflow run still in the read pool moves to the write pool
   // (the read pool is the next launch's write pool)
   if (klane && n > S && !(ovo & kOvoWr)) {
@@ -1227,7 +1244,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
 
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
   const int P = 1 << a.pat.buckets_log2;
-  const size_t dyn = ((size_t)(P + 1) * 4 + 15) & ~(size_t)15;
+  const size_t dyn = ((size_t)(P + a.nhot + 1) * 4 + 15) & ~(size_t)15;
   const dim3 g((unsigned)ntiles), b(kCfPartThreads);
   if (a.in_recs) {
     switch (a.cf.nw) {

@@ -135,6 +135,16 @@ struct PatternRT {
   bool sparse = false;
   uint64_t table_cap = 0;
   DevBuf tkey, tval, krev, kcount, dense;
+  // hot keys (hot.hip): keys that would make their bucket a straggler are
+  // matched by grid-wide scans; the walk reports candidates, diversion starts
+  // (sticky) once the device has put a key into a hot slot
+  bool hot = false;            // candidate collection on (closed-form path, P + kCfHotMax buckets fit)
+  bool hot_on = false;         // diversion active: hot arenas allocated
+  uint32_t hot_thresh = 0;     // records per key per launch that make a key hot
+  int hot_blocks = 0;
+  DevBuf hot_id, hot_key, hot_m, hot_gbase, hoff, cand, ncand, harr, hrow, hnb, bsum, bcnt, boff, hcm, hobase,
+      hot_active;
+  HostBuf hot_active_host;     // pinned: slots in use (read without a sync)
 };
 
 struct TimedLaunch {
@@ -490,7 +500,7 @@ int create_runtime(cep_app* a) {
         const int rw = 1 + std::max(p.nrec_a, p.nrec_b);
         for (int b = 0; b < 2 && ok; ++b)
           ok = dev_ensure(&rt.cf_recs[b], (size_t)cc * rw * 8 + 16, a->stream, false) &&
-               dev_ensure(&rt.cf_toff[b], (size_t)nt * ((1 << lg) + 1) * 2 + 16, a->stream, false);
+               dev_ensure(&rt.cf_toff[b], (size_t)nt * ((1 << lg) + kCfHotMax + 1) * 2 + 16, a->stream, false);
         if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
         const int plg = a->opt.pending_pool_log2 > 0 ? std::min(a->opt.pending_pool_log2, 30) : 20;
         rt.pool_cap = (int64_t)1 << plg;
@@ -503,6 +513,24 @@ int create_runtime(cep_app* a) {
         rt.extra_bound += rt.pool_cap;   // pool partials may complete too
         rt.cf = true;
         rt.cf_chunk = cc;
+        // hot keys: candidate lists now, the match arenas when first needed
+        if ((1 << lg) + kCfHotMax <= kCfMaxBuckets && !std::getenv("CEP_NO_HOT")) {
+          rt.hot_thresh = (uint32_t)std::max<int64_t>(256, cc >> 15);
+          ok = dev_ensure(&rt.hot_id, (size_t)kc * 2 + 16, a->stream, false) &&
+               dev_ensure(&rt.hot_key, kCfHotMax * 4, a->stream, false) &&
+               dev_ensure(&rt.hot_m, kCfHotMax * 4, a->stream, false) &&
+               dev_ensure(&rt.cand, kCfHotMax * 4 * 8, a->stream, false) &&
+               dev_ensure(&rt.ncand, 64, a->stream, false) && dev_ensure(&rt.hot_active, 64, a->stream, false) &&
+               host_ensure(&rt.hot_active_host, 64);
+          if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (hot keys)");
+          hipMemset(rt.hot_id.p, 0xff, (size_t)kc * 2 + 16);
+          hipMemset(rt.hot_key.p, 0xff, kCfHotMax * 4);
+          hipMemset(rt.hot_m.p, 0, kCfHotMax * 4);
+          hipMemset(rt.ncand.p, 0, 64);
+          hipMemset(rt.hot_active.p, 0, 64);
+          std::memset(rt.hot_active_host.p, 0, 64);
+          rt.hot = true;
+        }
       }
     }
     if (a->opt.sparse_keys && keyed) {
@@ -679,6 +707,29 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     pa.ntiles = (int32_t)ntiles;
     pa.err = (unsigned int*)a->err.p;
     if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
+    // hot keys: diversion starts once the device reported a slot in use (the
+    // pinned word is refreshed asynchronously after every walk)
+    const bool hot = rt.hot && !in_recs;
+    if (hot && !rt.hot_on && *(volatile uint32_t*)rt.hot_active_host.p > 0) {
+      const int rw = 1 + cf.nw;
+      const int64_t cc = rt.cf_chunk, ntmax = cc / kCfTile;
+      rt.hot_blocks = (int)((cc + kHotBlock - 1) / kHotBlock);
+      const bool ok = dev_ensure(&rt.hot_gbase, (kCfHotMax + 1) * 4, a->stream, false) &&
+                      dev_ensure(&rt.hoff, (size_t)kCfHotMax * ntmax * 4, a->stream, false) &&
+                      dev_ensure(&rt.harr, (size_t)cc * rw * 8, a->stream, false) &&
+                      dev_ensure(&rt.hrow, (size_t)cc * 4, a->stream, false) &&
+                      dev_ensure(&rt.hnb, (size_t)cc * 4, a->stream, false) &&
+                      dev_ensure(&rt.bsum, (size_t)rt.hot_blocks * 16, a->stream, false) &&
+                      dev_ensure(&rt.bcnt, (size_t)rt.hot_blocks * 4, a->stream, false) &&
+                      dev_ensure(&rt.boff, (size_t)rt.hot_blocks * 4, a->stream, false) &&
+                      dev_ensure(&rt.hcm, kCfHotMax * 3 * 4, a->stream, false) &&
+                      dev_ensure(&rt.hobase, 64, a->stream, false);
+      if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (hot-key arenas)");
+      rt.hot_on = true;
+    }
+    const bool divert = hot && rt.hot_on;
+    pa.hot_id = divert ? (const uint16_t*)rt.hot_id.p : nullptr;
+    pa.nhot = divert ? kCfHotMax : 0;
     if (overlap && rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
     {
       LaunchTimer t(a, CEP_K_CF_PARTITION, side);
@@ -707,6 +758,53 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     hipMemsetAsync(rt.pool_cur.p, 0, 8, a->stream);
     wa.out = out_args(o, q);
     wa.err = pa.err;
+    HotArgs ha{};
+    if (hot) {
+      ha.pat = rt.pa;
+      ha.cf = cf;
+      ha.recs = pa.recs;
+      ha.tile_off = pa.tile_off;
+      ha.ntiles = (int32_t)ntiles;
+      ha.chunk_base = (const int64_t*)rt.chunk_base[b].p;
+      ha.hot_id = (uint16_t*)rt.hot_id.p;
+      ha.hot_key = (int32_t*)rt.hot_key.p;
+      ha.hot_m = (uint32_t*)rt.hot_m.p;
+      ha.hot_gbase = (uint32_t*)rt.hot_gbase.p;
+      ha.hoff = (uint32_t*)rt.hoff.p;
+      ha.cand = (uint64_t*)rt.cand.p;
+      ha.ncand = (uint32_t*)rt.ncand.p;
+      ha.cand_cap = kCfHotMax * 4;
+      ha.thresh = rt.hot_thresh;
+      ha.harr = (uint64_t*)rt.harr.p;
+      ha.hrow = (uint32_t*)rt.hrow.p;
+      ha.hnb = (uint32_t*)rt.hnb.p;
+      ha.bsum = (uint32_t*)rt.bsum.p;
+      ha.bcnt = (uint32_t*)rt.bcnt.p;
+      ha.boff = (uint32_t*)rt.boff.p;
+      ha.hcm = (uint32_t*)rt.hcm.p;
+      ha.obase = (unsigned long long*)rt.hobase.p;
+      ha.max_blocks = rt.hot_blocks;
+      ha.khdr = wa.khdr;
+      ha.kslot = wa.kslot;
+      ha.kstride = wa.kstride;
+      ha.kext = wa.kext;
+      ha.pool_rd = wa.pool_rd;
+      ha.pool_wr = wa.pool_wr;
+      ha.pool_cursor = wa.pool_cursor;
+      ha.pool_cap = wa.pool_cap;
+      ha.key_rev = wa.key_rev;
+      ha.out = wa.out;
+      ha.active = (uint32_t*)rt.hot_active.p;
+      ha.err = pa.err;
+      wa.hot_cand = ha.cand;
+      wa.hot_ncand = ha.ncand;
+      wa.hot_thresh = rt.hot_thresh;
+      wa.hot_id = divert ? ha.hot_id : nullptr;
+    }
+    if (divert) {
+      LaunchTimer t(a, CEP_K_HOT);
+      launch_hot_match(ha, a->stream);
+    }
     wa.in_seq = in_recs ? in_recs + rows.row0 * in_rec_words + 1 : nullptr;
     wa.in_rec_words = in_rec_words;
     static const int ablate = std::getenv("CEP_ABLATE") ? std::atoi(std::getenv("CEP_ABLATE")) : 0;
@@ -718,6 +816,10 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     {
       LaunchTimer t(a, CEP_K_CF_WALK);
       launch_cf_walk(wa, P, a->stream);
+    }
+    if (hot) {
+      launch_hot_update(ha, divert ? 1 : 0, a->stream);
+      hipMemcpyAsync(rt.hot_active_host.p, rt.hot_active.p, 4, hipMemcpyDeviceToHost, a->stream);
     }
     rt.pool_side ^= 1;   // this launch's write pool holds every run now
     if (overlap) hipEventRecord(rt.walk_done[b], a->stream);
@@ -1008,6 +1110,21 @@ void cep_destroy(cep_app* a) {
           if (t[i] && t[i - 1]) sum[i] += (double)(t[i] - t[i - 1]);
       }
     }
+    {   // slowest blocks (stragglers): first stamp to the last one written
+      std::vector<std::pair<uint64_t, int>> dur;
+      for (int b = 0; b < nb; ++b) {
+        const uint64_t* t = &st[(size_t)b * 16];
+        uint64_t hi = 0;
+        for (int i = 0; i < 16; ++i) hi = std::max(hi, t[i]);
+        if (t[0] && hi > t[0]) dur.push_back({hi - t[0], b});
+      }
+      std::sort(dur.rbegin(), dur.rend());
+      std::fprintf(stderr, "[cep stamps] slowest walk blocks (ticks):");
+      for (size_t i = 0; i < dur.size() && i < 6; ++i) std::fprintf(stderr, " b%d=%llu", dur[i].second,
+                                                                   (unsigned long long)dur[i].first);
+      if (!dur.empty()) std::fprintf(stderr, " median=%llu", (unsigned long long)dur[dur.size() / 2].first);
+      std::fprintf(stderr, "\n");
+    }
     std::fprintf(stderr, "[cep stamps] walk window0 ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);
     std::fprintf(stderr, "\n[cep stamps] walk window1 (%d blocks):", n1);
@@ -1053,6 +1170,10 @@ void cep_destroy(cep_app* a) {
     dev_free(&p.pool[1]);
     dev_free(&p.pool_cur);
     for (DevBuf* b : {&p.tkey, &p.tval, &p.krev, &p.kcount, &p.dense}) dev_free(b);
+    for (DevBuf* b : {&p.hot_id, &p.hot_key, &p.hot_m, &p.hot_gbase, &p.hoff, &p.cand, &p.ncand, &p.harr, &p.hrow,
+                      &p.hnb, &p.bsum, &p.bcnt, &p.boff, &p.hcm, &p.hobase, &p.hot_active})
+      dev_free(b);
+    host_free(&p.hot_active_host);
     for (int b = 0; b < 2; ++b) {
       dev_free(&p.recs[b]);
       dev_free(&p.tile_off[b]);
@@ -1539,6 +1660,8 @@ int cep_stats(cep_app* a, cep_stats_t* s) {
   s->matches_out = a->matches_out;
   s->batches = a->batches;
   s->late_events = a->late_events;
+  for (auto& p : a->pats)
+    if (p.hot) s->hot_keys += *(volatile uint32_t*)p.hot_active_host.p;
   for (int i = 0; i < 16; ++i) {
     s->kernel_launches[i] = a->launches[i];
     s->kernel_ms[i] = a->kernel_ms[i];

@@ -251,8 +251,18 @@ struct CfPlan {
   int32_t bcol_phys[kMaxCaps];     // B record word c (SRC_REC + c) -> physical word, -1 = ts
 };
 
+// Hot keys (hot.hip): keys whose records would make their bucket a straggler
+// (Zipf-skewed streams) are diverted by k_cfpart into hot buckets P + h
+// (h < kCfHotMax, one per key) and matched by grid-wide scans instead of one
+// workgroup per bucket.
+constexpr int kCfHotMax = 1024;
+constexpr int kHotBlock = 2048;                     // hot records per scan block
+constexpr uint16_t kNotHot = 0xffff;
+
 struct CfPartArgs {
   RowsArgs rows;
+  const uint16_t* hot_id;      // dense key -> hot slot (kNotHot), nullptr: no diversion
+  int32_t nhot;                // hot buckets after the P key buckets (0 or kCfHotMax)
   PrefPlan pref;
   int32_t ts_slot;             // prefetch slot whose column IS the event-ts buffer (-1: none)
   // received shuffle records (cep_send_records): rows are wide records
@@ -285,11 +295,54 @@ struct CfWalkArgs {
   unsigned long long* pool_cursor;   // slots allocated in pool_wr (zeroed per launch)
   uint64_t pool_cap;           // slots per pool
   const uint64_t* key_rev;     // sparse keys: dense key -> partition value (nullptr: dense keys)
+  const uint16_t* hot_id;      // diversion active: hot keys are not this launch's (nullptr: none)
+  uint64_t* hot_cand;          // records << 32 | dense key of keys over hot_thresh this launch
+  uint32_t* hot_ncand;
+  uint32_t hot_thresh;         // 0: no candidate collection
   OutArgs out;
   const uint64_t* in_seq;      // received records: &record[row0].seq (global arrival numbers), else nullptr
   int32_t in_rec_words;
   uint64_t* stamps;
   int32_t ablate;              // diagnostics (CEP_ABLATE): bit 0 no emission, 1 no commit, 2 no rank/reload
+  unsigned int* err;
+};
+
+struct HotArgs {
+  PatternArgs pat;
+  CfPlan cf;
+  const uint64_t* recs;        // k_cfpart records (tile-major)
+  const uint16_t* tile_off;    // [P + kCfHotMax + 1][ntiles]
+  int32_t ntiles;
+  const int64_t* chunk_base;
+  uint16_t* hot_id;            // [key_capacity] dense key -> slot
+  int32_t* hot_key;            // [kCfHotMax] slot -> dense key (-1: free)
+  uint32_t* hot_m;             // [kCfHotMax] records this chunk
+  uint32_t* hot_gbase;         // [kCfHotMax + 1] exclusive prefix of hot_m (last: M)
+  uint32_t* hoff;              // [kCfHotMax][ntiles] a slot's records before tile t
+  uint64_t* cand;              // walk candidates: records << 32 | dense key
+  uint32_t* ncand;
+  uint32_t cand_cap;
+  uint32_t thresh;
+  uint64_t* harr;              // hot records, grouped by slot, arrival order
+  uint32_t* hrow;              // chunk-relative row of each hot record
+  uint32_t* hnb;               // next B of the slot after each record (kNoPos: none)
+  uint32_t* bsum;              // per block: first slot, first B of it (incl.), last slot, carry
+  uint32_t* bcnt;              // per block: record matches
+  uint32_t* boff;
+  uint32_t* hcm;               // per slot: carried partials completed, first completed index
+  unsigned long long* obase;   // [0]: output base, [1]: carried rows total
+  int32_t max_blocks;
+  uint32_t* khdr;
+  uint64_t* kslot;
+  int64_t kstride;
+  uint64_t* kext;
+  const uint64_t* pool_rd;
+  uint64_t* pool_wr;
+  unsigned long long* pool_cursor;
+  uint64_t pool_cap;
+  const uint64_t* key_rev;
+  OutArgs out;
+  uint32_t* active;            // out: slots in use after the update
   unsigned int* err;
 };
 
@@ -337,6 +390,8 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_keymap(const KeyMapArgs& a, hipStream_t s);
 void launch_route_keys(const RouteKeyArgs& a, hipStream_t s);
+void launch_hot_match(const HotArgs& a, hipStream_t s);
+void launch_hot_update(const HotArgs& a, int diverted, hipStream_t s);
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

@@ -29,7 +29,7 @@ TYPE_NAMES = {INT: "int", LONG: "long", FLOAT: "float", DOUBLE: "double",
 NUMPY_DTYPES = {INT: "int32", LONG: "int64", FLOAT: "float32",
                 DOUBLE: "float64", BOOL: "uint8", STRING: "int32"}
 
-K_FILTER, K_PARTITION, K_WALK, K_ROUTE, K_ORDER, K_AGG, K_OTHER, K_CF_PARTITION, K_CF_WALK = range(9)
+K_FILTER, K_PARTITION, K_WALK, K_ROUTE, K_ORDER, K_AGG, K_OTHER, K_CF_PARTITION, K_CF_WALK, K_HOT = range(10)
 
 
 # ---- exceptions mirroring the reference ---------------------------------
@@ -116,7 +116,7 @@ class cep_stats_t(C.Structure):
     _fields_ = [("events_in", C.c_int64), ("matches_out", C.c_int64),
                 ("batches", C.c_int64), ("kernel_launches", C.c_int64 * 16),
                 ("kernel_ms", C.c_double * 16), ("kernel_timed", C.c_int64 * 16),
-                ("late_events", C.c_int64)]
+                ("late_events", C.c_int64), ("hot_keys", C.c_int64)]
 
 
 EMIT_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(cep_rows))

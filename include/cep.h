@@ -139,13 +139,15 @@ typedef struct {
   double kernel_ms[16];       /* with cep_options.profile: summed HIP-event time */
   int64_t kernel_timed[16];   /* launches kernel_ms covers (profile = k: every k-th) */
   int64_t late_events;        /* rows dropped by cep_watermark as late (ts before an earlier release) */
+  int64_t hot_keys;           /* closed-form path: keys matched by the hot-key kernels (hot.hip) */
 } cep_stats_t;
 
 /* Kernel kinds indexing cep_stats_t arrays. */
 enum {
   CEP_K_FILTER = 0, CEP_K_PARTITION = 1, CEP_K_WALK = 2, CEP_K_ROUTE = 3,
   CEP_K_ORDER = 4, CEP_K_AGG = 5, CEP_K_OTHER = 6,
-  CEP_K_CF_PARTITION = 7, CEP_K_CF_WALK = 8   /* closed-form fast path (k_cfpart / k_cfwalk) */
+  CEP_K_CF_PARTITION = 7, CEP_K_CF_WALK = 8,  /* closed-form fast path (k_cfpart / k_cfwalk) */
+  CEP_K_HOT = 9                               /* hot-key matching (hot.hip, one entry per chunk) */
 };
 
 /* ---- plan-level calls (no device needed) ------------------------------ */

@@ -1,0 +1,117 @@
+"""Hot keys on the closed-form path (csrc/hot.hip) vs the C oracle.
+
+Keys whose records would make their bucket a straggler are diverted by
+k_cfpart into hot buckets and matched by grid-wide scans (k_hot_*), while
+the walk keeps the rest; keys move between the two as the stream's skew
+changes.  Every case compares the rows and their per-key order with
+oracle/cep_oracle.c over the same events (BASELINE.md §3 Zipf variant and
+harsher shapes: keys that go cold and hot again, hot keys whose B's are rare
+so their pending lists spill to the overflow pool, sparse 64-bit key values).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cep_oracle as CO  # noqa: E402
+import flink_siddhi as fs  # noqa: E402
+from flink_siddhi import _lib as L  # noqa: E402
+from flink_siddhi import workload  # noqa: E402
+from test_gpu_geometry import F, assert_same_per_key  # noqa: E402
+
+
+def run_batches(batches, keys, rate, plan, chunk, key_value=None, **opts):
+    """batches: [(first, n, key remap table or None)] -> (device rows as numpy, stats)."""
+    import torch
+    rt = fs.SiddhiAppRuntime(plan, chunk_events=chunk, ordered_output=0, key_capacity=keys, **opts)
+    parts = []
+    for first, n, table in batches:
+        d = workload.generate_device(first, n, keys, rate=rate)
+        if table is not None:
+            d["k"] = torch.from_numpy(table).cuda()[d["k"].long()]
+        k = d["k"] if key_value is None else key_value(d["k"])
+        rt.send("A", d["ts"], [k, d["ts"], d["id"], d["price"]], streams=d["stream"])
+        ts, seq, cols = rt.output_tensors("O")
+        rt.flush()
+        parts.append((ts, seq, cols))
+    torch.cuda.synchronize()
+    st = rt.stats()
+    rt.shutdown()
+    cat = lambda i: torch.cat([p[2][i] for p in parts]).cpu().numpy()  # noqa: E731
+    out = {"k": cat(0), "p1": cat(1), "p2": cat(2), "t": cat(3),
+           "ts": torch.cat([p[0] for p in parts]).cpu().numpy(),
+           "seq": torch.cat([p[1] for p in parts]).cpu().numpy()}
+    return out, st
+
+
+def oracle_batches(batches, keys, rate, g, within):
+    total = sum(n for _, n, _ in batches)
+    w = CO.generate(0, total, keys, rate=rate, threads=16)
+    for first, n, table in batches:
+        if table is not None:
+            w["k"][first:first + n] = table[w["k"][first:first + n]]
+    po = CO.PatternOracle(keys, F, g, every=True, within=within)
+    a, b, m = po.run(w)
+    return {"k": w["k"][a], "p1": w["price"][a], "p2": w["price"][b], "t": w["ts"][b],
+            "ts": w["ts"][b], "seq": b}, w
+
+
+def plan_with(g_text, within_text):
+    return (workload.PATTERN_PLAN.replace("id % 7 == 0", g_text)
+            .replace("within 10 sec", within_text))
+
+
+def test_hot_keys_come_and_go():
+    # Zipf, then uniform (the hot keys go cold and are released), then Zipf
+    # with other hot keys; 1 Mi-event chunks make keys with > 256 records per
+    # chunk hot
+    keys, rate, n = 1 << 16, 400, 1 << 21
+    za = workload.zipf_map(keys, seed=7)
+    zb = workload.zipf_map(keys, seed=99)
+    tables = [za, za, za, None, None, zb, zb]
+    batches = [(i * n, n, t) for i, t in enumerate(tables)]
+    got, st = run_batches(batches, keys, rate, workload.PATTERN_PLAN, 1 << 20)
+    want, _ = oracle_batches(batches, keys, rate, CO.cond(("id", 7, "==", 0)), 10000)
+    assert st.kernel_launches[L.K_HOT] > 0, "hot-key path never engaged"
+    assert st.kernel_launches[L.K_CF_WALK] > 0
+    assert_same_per_key(got, want)
+    assert len(want["k"]) > 300_000
+
+
+def test_hot_keys_with_rare_b_spill_to_pool():
+    # g true only for id == 0 (1 in 50 B's): a hot key's A's pile up for up to W, past the
+    # 16 inline slots; the hot commit writes the overflow runs
+    keys, rate, n = 1 << 14, 200, 1 << 21
+    z = workload.zipf_map(keys, seed=3)
+    batches = [(i * n, n, z) for i in range(4)]
+    plan = plan_with("id % 97 == 0", "within 1 sec")
+    got, st = run_batches(batches, keys, rate, plan, 1 << 20)
+    want, _ = oracle_batches(batches, keys, rate, CO.cond(("id", 97, "==", 0)), 1000)
+    assert st.kernel_launches[L.K_HOT] > 0
+    assert_same_per_key(got, want)
+    assert len(want["k"]) > 10_000
+
+
+def test_hot_keys_sparse_long_values():
+    # sparse_keys: 64-bit partition values through the device key map; the
+    # hot rows output the original values
+    keys, rate, n = 1 << 16, 400, 1 << 21
+    z = workload.zipf_map(keys, seed=11)
+    batches = [(i * n, n, z) for i in range(3)]
+    base, mul = 1 << 40, 7919
+    got, st = run_batches(batches, keys, rate, workload.PATTERN_PLAN.replace("k int", "k long"), 1 << 20,
+                          key_value=lambda k: k.long() * mul + base, sparse_keys=1)
+    want, _ = oracle_batches(batches, keys, rate, CO.cond(("id", 7, "==", 0)), 10000)
+    assert st.kernel_launches[L.K_HOT] > 0
+    got["k"] = ((got["k"].astype(np.int64) - base) // mul).astype(np.int32)
+    assert_same_per_key(got, want)
+
+
+def test_uniform_stream_never_diverts():
+    # no key reaches the threshold: the hot kernels never run
+    keys, rate, n = 1 << 16, 400, 1 << 21
+    batches = [(i * n, n, None) for i in range(3)]
+    got, st = run_batches(batches, keys, rate, workload.PATTERN_PLAN, 1 << 20)
+    want, _ = oracle_batches(batches, keys, rate, CO.cond(("id", 7, "==", 0)), 10000)
+    assert st.kernel_launches[L.K_HOT] == 0 and st.hot_keys == 0
+    assert_same_per_key(got, want)
