@@ -145,6 +145,7 @@ struct PatternRT {
   DevBuf hot_id, hot_key, hot_m, hot_gbase, hoff, cand, ncand, harr, hrow, hnb, bsum, bcnt, boff, hcm, hobase,
       hot_active;
   HostBuf hot_active_host;     // pinned: slots in use (read without a sync)
+  hipEvent_t hot_fork = nullptr, hot_join = nullptr;   // hot kernels on the side stream, beside the walk
 };
 
 struct TimedLaunch {
@@ -522,6 +523,8 @@ int create_runtime(cep_app* a) {
                dev_ensure(&rt.cand, kCfHotMax * 4 * 8, a->stream, false) &&
                dev_ensure(&rt.ncand, 64, a->stream, false) && dev_ensure(&rt.hot_active, 64, a->stream, false) &&
                host_ensure(&rt.hot_active_host, 64);
+          ok = ok && hipEventCreateWithFlags(&rt.hot_fork, hipEventDisableTiming) == hipSuccess &&
+               hipEventCreateWithFlags(&rt.hot_join, hipEventDisableTiming) == hipSuccess;
           if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (hot keys)");
           hipMemset(rt.hot_id.p, 0xff, (size_t)kc * 2 + 16);
           hipMemset(rt.hot_key.p, 0xff, kCfHotMax * 4);
@@ -801,9 +804,20 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       wa.hot_thresh = rt.hot_thresh;
       wa.hot_id = divert ? ha.hot_id : nullptr;
     }
+    // the hot kernels run on the side stream beside the walk: disjoint keys,
+    // shared output / pool cursors are atomics (CEP_HOT_SERIAL=1: main stream)
+    static const bool hot_serial = std::getenv("CEP_HOT_SERIAL") != nullptr;
+    hipStream_t hs = hot_serial ? a->stream : a->side;
     if (divert) {
-      LaunchTimer t(a, CEP_K_HOT);
-      launch_hot_match(ha, a->stream);
+      if (!hot_serial) {
+        hipEventRecord(rt.hot_fork, a->stream);
+        hipStreamWaitEvent(hs, rt.hot_fork, 0);
+      }
+      {
+        LaunchTimer t(a, CEP_K_HOT, hs);
+        launch_hot_match(ha, hs);
+      }
+      if (!hot_serial) hipEventRecord(rt.hot_join, hs);
     }
     wa.in_seq = in_recs ? in_recs + rows.row0 * in_rec_words + 1 : nullptr;
     wa.in_rec_words = in_rec_words;
@@ -818,6 +832,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       launch_cf_walk(wa, P, a->stream);
     }
     if (hot) {
+      if (divert && !hot_serial) hipStreamWaitEvent(a->stream, rt.hot_join, 0);
       launch_hot_update(ha, divert ? 1 : 0, a->stream);
       hipMemcpyAsync(rt.hot_active_host.p, rt.hot_active.p, 4, hipMemcpyDeviceToHost, a->stream);
     }
@@ -1174,6 +1189,8 @@ void cep_destroy(cep_app* a) {
                       &p.hnb, &p.bsum, &p.bcnt, &p.boff, &p.hcm, &p.hobase, &p.hot_active})
       dev_free(b);
     host_free(&p.hot_active_host);
+    if (p.hot_fork) hipEventDestroy(p.hot_fork);
+    if (p.hot_join) hipEventDestroy(p.hot_join);
     for (int b = 0; b < 2; ++b) {
       dev_free(&p.recs[b]);
       dev_free(&p.tile_off[b]);

@@ -153,7 +153,9 @@ __global__ __launch_bounds__(kHT) void k_hot_base(HotArgs a) {
 
 // ---- per tile: hot segments sorted by (slot, row) -> the slot-grouped array
 __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
-  __shared__ uint64_t sk[kCfTile];
+  __shared__ uint32_t sk[kCfTile];           // slot << 13 | row (rows are unique in a tile)
+  __shared__ uint16_t imap[kCfTile];         // row -> record index in the tile's hot region
+  __shared__ uint32_t sbase[kCfHotMax], sstart[kCfHotMax];
   const int64_t t = blockIdx.x;
   const int64_t nt = a.ntiles;
   const int P = 1 << a.pat.buckets_log2;
@@ -166,10 +168,11 @@ __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
   while (N < cnt) N <<= 1;
   const uint64_t* tr = a.recs + (t * kCfTile + r0) * RW;
   for (uint32_t i = threadIdx.x; i < N; i += kHT) {
-    uint64_t k = ~0ull;
+    uint32_t k = 0xffffffffu;
     if (i < cnt) {
       const uint64_t w0 = tr[(int64_t)i * RW];
-      k = ((uint64_t)h_slot(w0) << 26) | ((uint64_t)h_row(w0) << 13) | i;
+      k = (h_slot(w0) << 13) | h_row(w0);
+      imap[h_row(w0)] = (uint16_t)i;
     }
     sk[i] = k;
   }
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
       for (uint32_t i = threadIdx.x; i < N; i += kHT) {
         const uint32_t ixj = i ^ j;
         if (ixj > i) {
-          const uint64_t x = sk[i], y = sk[ixj];
+          const uint32_t x = sk[i], y = sk[ixj];
           const bool asc = (i & k) == 0;
           if ((x > y) == asc) {
             sk[i] = y;
@@ -191,31 +194,20 @@ __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
       lds_barrier();
     }
   }
-  // run starts (first position of each slot): the run's destination base in
-  // the key's high bits (one global lookup per run, not per record)
+  // run starts: each slot's first position and destination base
   for (uint32_t p = threadIdx.x; p < cnt; p += kHT) {
-    const uint64_t k = sk[p];
-    const uint32_t h = (uint32_t)(k >> 26) & 0x3ffu;
-    if (p == 0 || ((uint32_t)(sk[p - 1] >> 26) & 0x3ffu) != h) {
-      const uint32_t base = a.hot_gbase[h] + a.hoff[(int64_t)h * nt + t];
-      sk[p] = k | ((uint64_t)base << 38);
+    const uint32_t h = sk[p] >> 13;
+    if (p == 0 || (sk[p - 1] >> 13) != h) {
+      sstart[h] = p;
+      sbase[h] = a.hot_gbase[h] + a.hoff[(int64_t)h * nt + t];
     }
   }
   lds_barrier();
   for (uint32_t p = threadIdx.x; p < cnt; p += kHT) {
-    const uint64_t k = sk[p];
-    const uint32_t i = (uint32_t)k & 0x1fffu;
-    const uint32_t h = (uint32_t)(k >> 26) & 0x3ffu;
-    const uint32_t row = (uint32_t)(k >> 13) & 0x1fffu;
-    // the run start: lower bound of slot h (keys are sorted by slot first)
-    uint32_t lo = 0, hi = p;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (((uint32_t)(sk[mid] >> 26) & 0x3ffu) < h) lo = mid + 1;
-      else hi = mid;
-    }
-    const uint32_t dest = (uint32_t)(sk[lo] >> 38) + (p - lo);
-    const uint64_t* src = tr + (int64_t)i * RW;
+    const uint32_t k = sk[p];
+    const uint32_t h = k >> 13, row = k & 0x1fffu;
+    const uint32_t dest = sbase[h] + (p - sstart[h]);
+    const uint64_t* src = tr + (int64_t)imap[row] * RW;
     uint64_t* dst = a.harr + (int64_t)dest * RW;
     for (int w = 0; w < RW; ++w) dst[w] = src[w];
     a.hrow[dest] = (uint32_t)t * (uint32_t)kCfTile + row;
