@@ -11,7 +11,7 @@ rm -rf "$R/gpurun_out/pmc"
 for grp in "${GROUPS_DEFAULT[@]}"; do
   i=$((i+1))
   echo "pass $i: $grp"
-  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$R/gpurun_out/pmc" -o "pass$i" -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_pass$i.log" 2>&1 || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$R/gpurun_out/pmc" -o "pass$i" -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/pmc_pass$i.txt" 2>&1 || exit $?
 done
 python3 "$R/scripts/pmc_summary.py" "$R/gpurun_out/pmc" "$R/gpurun_out/${1:-pmc_summary.json}"
 exit 0
