@@ -712,7 +712,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
     // hot keys: diversion starts once the device reported a slot in use (the
     // pinned word is refreshed asynchronously after every walk)
-    const bool hot = rt.hot && !in_recs;
+    const bool hot = rt.hot;
     if (hot && !rt.hot_on && *(volatile uint32_t*)rt.hot_active_host.p > 0) {
       const int rw = 1 + cf.nw;
       const int64_t cc = rt.cf_chunk, ntmax = cc / kCfTile;
@@ -798,6 +798,8 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       ha.key_rev = wa.key_rev;
       ha.out = wa.out;
       ha.active = (uint32_t*)rt.hot_active.p;
+      ha.in_seq = in_recs ? in_recs + rows.row0 * in_rec_words + 1 : nullptr;
+      ha.in_rec_words = in_rec_words;
       ha.err = pa.err;
       wa.hot_cand = ha.cand;
       wa.hot_ncand = ha.ncand;

@@ -68,6 +68,12 @@ __device__ __forceinline__ uint32_t hot_total(const HotArgs& a) { return a.hot_g
 
 __device__ __forceinline__ bool within_w(int64_t W, int64_t d) { return W < 0 || (d < 0 ? -d : d) <= W; }
 
+// Arrival number of the record at chunk row r (received shuffle records carry
+// their global number; local rows are numbered from the chunk base).
+__device__ __forceinline__ int64_t row_seq_of(const HotArgs& a, int64_t seq_base, uint32_t r) {
+  return a.in_seq ? (int64_t)a.in_seq[(int64_t)r * a.in_rec_words] : seq_base + (int64_t)r;
+}
+
 // One output row (as k_cfwalk's cf_emit).
 __device__ __forceinline__ void hot_emit_row(const HotArgs& a, unsigned long long pos, int64_t kf,
                                              uint64_t acap0, uint64_t acap1, uint64_t b0, uint64_t b1,
@@ -456,7 +462,7 @@ __global__ __launch_bounds__(kHT) void k_hot_emit(HotArgs a) {
       a_caps(a, r, ats, &x0, &x1);
       const int64_t kf = a.hot_key[h_slot(r[0])];
       hot_emit_row(a, base + off, kf, x0, x1, a.cf.nw > 0 ? rb[1] : 0ull, a.cf.nw > 1 ? rb[2] : 0ull, bts,
-                   seq_base + (int64_t)a.hrow[nbv]);
+                   row_seq_of(a, seq_base, a.hrow[nbv]));
     }
     base += total;
   }
@@ -540,7 +546,7 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
     for (uint32_t j = lane; j < cm; j += 64) {
       const int js = (int)(cfirst + j);
       hot_emit_row(a, a.obase[0] + cm_off + j, kf, c1 ? slot_word(a, kidx, js, 2, ovoff) : 0ull,
-                   c2 ? slot_word(a, kidx, js, 3, ovoff) : 0ull, b0, b1, bts, seq_base + (int64_t)a.hrow[fb]);
+                   c2 ? slot_word(a, kidx, js, 3, ovoff) : 0ull, b0, b1, bts, row_seq_of(a, seq_base, a.hrow[fb]));
     }
   }
   // the new list: (no B) the carried partials minus the pruned prefix, then

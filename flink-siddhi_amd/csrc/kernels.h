@@ -343,6 +343,8 @@ struct HotArgs {
   const uint64_t* key_rev;
   OutArgs out;
   uint32_t* active;            // out: slots in use after the update
+  const uint64_t* in_seq;      // received shuffle records: &record[row0].seq, else nullptr
+  int32_t in_rec_words;
   unsigned int* err;
 };
 

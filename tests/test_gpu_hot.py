@@ -115,3 +115,55 @@ def test_uniform_stream_never_diverts():
     want, _ = oracle_batches(batches, keys, rate, CO.cond(("id", 7, "==", 0)), 10000)
     assert st.kernel_launches[L.K_HOT] == 0 and st.hot_keys == 0
     assert_same_per_key(got, want)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_hot_keys_on_shuffle_owners(world):
+    # owners of the key shuffle (cep_send_records: k_cfpart from received
+    # records) divert their hot keys too; the hot rows carry the global
+    # arrival numbers of the received records
+    import torch
+    keys, rate, n_per, steps = 1 << 16, 400, 1 << 20, 4
+    z = torch.from_numpy(workload.zipf_map(keys, seed=5)).cuda()
+    plan = workload.PATTERN_PLAN
+    rts = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=1 << 20,
+                               key_capacity=keys, ordered_output=0) for r in range(world)]
+    parts = [[] for _ in range(world)]
+    for s in range(steps):
+        segs = [[] for _ in range(world)]
+        for src in range(world):
+            first = (s * world + src) * n_per
+            d = workload.generate_device(first, n_per, keys, rate=rate)
+            d["k"] = z[d["k"].long()]
+            recs, counts = rts[src].route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
+                                          seq0=first, streams=d["stream"])
+            off = np.concatenate([[0], np.cumsum(counts)])
+            for r in range(world):
+                segs[r].append(recs[off[r]:off[r + 1]].clone())
+        for r in range(world):
+            recv = torch.cat(segs[r], dim=0)
+            rts[r].send_records(recv, recv.shape[0], n_per)
+            ts, seq, cols = rts[r].output_tensors("O")
+            rts[r].flush()
+            parts[r].append((ts, seq, cols))
+    torch.cuda.synchronize()
+    hot = sum(rt.stats().kernel_launches[L.K_HOT] for rt in rts)
+    got = {c: [] for c in ("k", "p1", "p2", "t", "ts", "seq")}
+    for r in range(world):
+        for ts, seq, cols in parts[r]:
+            for c, v in zip(("k", "p1", "p2", "t"), cols):
+                got[c].append(v.cpu().numpy())
+            got["ts"].append(ts.cpu().numpy())
+            got["seq"].append(seq.cpu().numpy())
+    got = {c: np.concatenate(v) for c, v in got.items()}
+    for rt in rts:
+        rt.shutdown()
+    total = steps * world * n_per
+    w = CO.generate(0, total, keys, rate=rate, threads=16)
+    w["k"] = z.cpu().numpy()[w["k"]]
+    po = CO.PatternOracle(keys, F, CO.cond(("id", 7, "==", 0)), every=True, within=10000)
+    a, b, m = po.run(w)
+    want = {"k": w["k"][a], "p1": w["price"][a], "p2": w["price"][b], "t": w["ts"][b],
+            "ts": w["ts"][b], "seq": b}
+    assert hot > 0, "hot-key path never engaged on the owners"
+    assert_same_per_key(got, want)
