@@ -516,7 +516,8 @@ int create_runtime(cep_app* a) {
         rt.cf_chunk = cc;
         // hot keys: candidate lists now, the match arenas when first needed
         if ((1 << lg) + kCfHotMax <= kCfMaxBuckets && !std::getenv("CEP_NO_HOT")) {
-          rt.hot_thresh = (uint32_t)std::max<int64_t>(256, cc >> 15);
+          rt.hot_thresh = (uint32_t)std::max<int64_t>(256, cc >> 16);
+          if (const char* e = std::getenv("CEP_HOT_THRESH")) rt.hot_thresh = (uint32_t)std::max(16, std::atoi(e));
           ok = dev_ensure(&rt.hot_id, (size_t)kc * 2 + 16, a->stream, false) &&
                dev_ensure(&rt.hot_key, kCfHotMax * 4, a->stream, false) &&
                dev_ensure(&rt.hot_m, kCfHotMax * 4, a->stream, false) &&
@@ -800,6 +801,8 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       ha.active = (uint32_t*)rt.hot_active.p;
       ha.in_seq = in_recs ? in_recs + rows.row0 * in_rec_words + 1 : nullptr;
       ha.in_rec_words = in_rec_words;
+      static const int hot_ablate = std::getenv("CEP_HOT_ABLATE") ? std::atoi(std::getenv("CEP_HOT_ABLATE")) : 0;
+      ha.ablate = hot_ablate;
       ha.err = pa.err;
       wa.hot_cand = ha.cand;
       wa.hot_ncand = ha.ncand;

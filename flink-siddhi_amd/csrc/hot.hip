@@ -157,11 +157,16 @@ __global__ __launch_bounds__(kHT) void k_hot_base(HotArgs a) {
   }
 }
 
-// ---- per tile: hot segments sorted by (slot, row) -> the slot-grouped array
+// ---- per tile: hot segments in row order -> the slot-grouped array.  The
+// tile's hot region is already grouped by slot (k_cfpart's bucket order);
+// inside a slot's segment a record's rank is the number of the segment's
+// records with a smaller row (rows are unique in a tile).  Segments are
+// short except for the very hottest keys, so this costs far less than
+// sorting the region.
 __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
-  __shared__ uint32_t sk[kCfTile];           // slot << 13 | row (rows are unique in a tile)
-  __shared__ uint16_t imap[kCfTile];         // row -> record index in the tile's hot region
-  __shared__ uint32_t sbase[kCfHotMax], sstart[kCfHotMax];
+  __shared__ uint16_t sslot[kCfTile], srow[kCfTile];
+  __shared__ uint32_t sbase[kCfHotMax];
+  __shared__ uint16_t sstart[kCfHotMax], send[kCfHotMax];
   const int64_t t = blockIdx.x;
   const int64_t nt = a.ntiles;
   const int P = 1 << a.pat.buckets_log2;
@@ -170,50 +175,32 @@ __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
   const uint32_t r1 = a.tile_off[(int64_t)(P + kCfHotMax) * nt + t];
   const uint32_t cnt = r1 - r0;
   if (cnt == 0) return;
-  uint32_t N = 2;
-  while (N < cnt) N <<= 1;
   const uint64_t* tr = a.recs + (t * kCfTile + r0) * RW;
-  for (uint32_t i = threadIdx.x; i < N; i += kHT) {
-    uint32_t k = 0xffffffffu;
-    if (i < cnt) {
-      const uint64_t w0 = tr[(int64_t)i * RW];
-      k = (h_slot(w0) << 13) | h_row(w0);
-      imap[h_row(w0)] = (uint16_t)i;
-    }
-    sk[i] = k;
+  for (uint32_t i = threadIdx.x; i < cnt; i += kHT) {
+    const uint64_t w0 = tr[(int64_t)i * RW];
+    sslot[i] = (uint16_t)h_slot(w0);
+    srow[i] = (uint16_t)h_row(w0);
   }
   lds_barrier();
-  // bitonic sort (ascending) of N keys
-  for (uint32_t k = 2; k <= N; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < N; i += kHT) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const uint32_t x = sk[i], y = sk[ixj];
-          const bool asc = (i & k) == 0;
-          if ((x > y) == asc) {
-            sk[i] = y;
-            sk[ixj] = x;
-          }
-        }
-      }
-      lds_barrier();
-    }
-  }
-  // run starts: each slot's first position and destination base
   for (uint32_t p = threadIdx.x; p < cnt; p += kHT) {
-    const uint32_t h = sk[p] >> 13;
-    if (p == 0 || (sk[p - 1] >> 13) != h) {
-      sstart[h] = p;
+    const uint32_t h = sslot[p];
+    if (p == 0 || sslot[p - 1] != h) {
+      sstart[h] = (uint16_t)p;
       sbase[h] = a.hot_gbase[h] + a.hoff[(int64_t)h * nt + t];
     }
+    if (p + 1 == cnt || sslot[p + 1] != h) send[h] = (uint16_t)(p + 1 - 1);   // last position
   }
   lds_barrier();
   for (uint32_t p = threadIdx.x; p < cnt; p += kHT) {
-    const uint32_t k = sk[p];
-    const uint32_t h = k >> 13, row = k & 0x1fffu;
-    const uint32_t dest = sbase[h] + (p - sstart[h]);
-    const uint64_t* src = tr + (int64_t)imap[row] * RW;
+    const uint32_t h = sslot[p];
+    const uint32_t row = srow[p];
+    const uint32_t s0 = sstart[h], s1 = (uint32_t)send[h] + 1;
+    uint32_t rank = 0;
+    if (!(a.ablate & 1))
+      for (uint32_t q = s0; q < s1; ++q) rank += srow[q] < row ? 1u : 0u;
+    const uint32_t dest = sbase[h] + rank;
+    if (a.ablate & 2) continue;
+    const uint64_t* src = tr + (int64_t)p * RW;
     uint64_t* dst = a.harr + (int64_t)dest * RW;
     for (int w = 0; w < RW; ++w) dst[w] = src[w];
     a.hrow[dest] = (uint32_t)t * (uint32_t)kCfTile + row;

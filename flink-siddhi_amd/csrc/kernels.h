@@ -345,6 +345,7 @@ struct HotArgs {
   uint32_t* active;            // out: slots in use after the update
   const uint64_t* in_seq;      // received shuffle records: &record[row0].seq, else nullptr
   int32_t in_rec_words;
+  int32_t ablate;              // diagnostics (CEP_HOT_ABLATE, wrong results): 1 no gather sort, 2 no gather copy
   unsigned int* err;
 };
 
