@@ -407,9 +407,11 @@ def main():
     send_fn = rt.send_records if pattern else rt.send_rows
 
     def route(d, j):
+        # inputs were generated before the timed region (synchronized): the
+        # route of step s+1 need not queue behind the exchange on torch's stream
         recs, counts = route_fn("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
                                 world, seq0=d["first"], streams=d["stream"],
-                                out=bufs.get(("send", j)))
+                                out=bufs.get(("send", j)), wait=False)
         bufs[("send", j)] = recs
         return recs, counts
 

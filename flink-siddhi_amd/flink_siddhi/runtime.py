@@ -254,11 +254,14 @@ class SiddhiAppRuntime:
         return w
 
     def route(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int,
-              streams=None, out=None):
+              streams=None, out=None, wait: bool = True):
         """Sender side of the key shuffle: evaluates the pattern's state
         filters on a device batch (push-down) and returns (records, counts):
         a uint64 device tensor [n, record_words] grouped by owner shard
-        (key % world) in arrival order, and the per-owner record counts."""
+        (key % world) in arrival order, and the per-owner record counts.
+        The routing is complete on return (the counts are read back).
+        wait=False: the inputs are known to be ready (produced before an
+        earlier sync), so routing does not queue behind torch's stream."""
         import torch
         h = self.input_handle(stream_id)
         defs = self.stream_definition(stream_id)
@@ -281,10 +284,10 @@ class SiddhiAppRuntime:
         b = L.cep_batch(n=n, ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
                         cols=ptrs, on_device=1)
         counts = (C.c_int64 * world)()
-        self._wait_producer(ts)
+        if wait:
+            self._wait_producer(ts)
         self._check(self._lib.cep_route_batch(self._h, C.byref(b), world, seq0,
                                               C.c_void_p(out.data_ptr()), out.shape[0], counts))
-        self._signal_consumer(ts)
         return out, [int(c) for c in counts]
 
     def partition_channels(self, stream_id: str, ts, cols: Sequence, key_field: Optional[str],
@@ -324,7 +327,7 @@ class SiddhiAppRuntime:
         return w
 
     def route_rows(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int,
-                   streams=None, out=None):
+                   streams=None, out=None, wait: bool = True):
         """Sender side of the row shuffle (multi-query apps, no push-down):
         (rows, counts) — an int64 device tensor [n, row_words] grouped by
         owner in arrival order, and the per-owner row counts."""
@@ -350,10 +353,10 @@ class SiddhiAppRuntime:
         b = L.cep_batch(n=n, ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
                         cols=ptrs, on_device=1)
         counts = (C.c_int64 * world)()
-        self._wait_producer(ts)
+        if wait:
+            self._wait_producer(ts)
         self._check(self._lib.cep_route_rows(self._h, C.byref(b), world, seq0,
                                              C.c_void_p(out.data_ptr()), out.shape[0], counts))
-        self._signal_consumer(ts)
         return out, [int(c) for c in counts]
 
     def send_rows(self, rows, n: int, events_represented: int = 0, signal: bool = True):
