@@ -340,7 +340,8 @@ def main():
     elif config5:
         plan = workload.config5_plan()
         opts = dict(device=local, key_capacity=(args.keys + world - 1) // world, key_stride=world,
-                    key_offset=rank, pending_slots=4, profile=PROFILE_EVERY, ordered_output=0)
+                    key_offset=rank, pending_slots=4, profile=PROFILE_EVERY, ordered_output=0,
+                    chunk_events=min(args.chunk, 1 << 24))
     else:
         plan = workload.FILTER_PLAN
         opts = dict(device=local, profile=PROFILE_EVERY, ordered_output=0)

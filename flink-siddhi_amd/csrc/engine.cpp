@@ -438,9 +438,13 @@ int create_runtime(cep_app* a) {
         !dev_ensure(&rt.chunk_base[1], 64, a->stream, false))
       return fail(a, CEP_E_DEVICE, "out of device memory (pattern state)");
     hipMemset(rt.khdr.p, 0, (size_t)rt.kstride * 4);
+    // the walk build decides the chunk cap (its LDS segment tables)
+    bool walk_vm = q.g_in_walk || agg || q.nfa;
+    for (auto& it : q.select) walk_vm |= it.src == SRC_VM;
     int64_t chunk = a->opt.chunk_events;
     chunk = std::max<int64_t>(chunk, kPartThreads * kPartItems);
-    chunk = std::min<int64_t>(chunk, (int64_t)kWalkMaxTiles * kPartThreads * kPartItems);
+    chunk = std::min<int64_t>(chunk, (int64_t)(walk_vm ? kWalkMaxTiles : kWalkMaxTiles / 4) *
+                                         kPartThreads * kPartItems);
     chunk = (chunk / (kPartThreads * kPartItems)) * (kPartThreads * kPartItems);
     rt.chunk = chunk;
     const int64_t ntiles = chunk / (kPartThreads * kPartItems);
@@ -479,8 +483,7 @@ int create_runtime(cep_app* a) {
       }
     }
     // group-by and N-state / sequence walks live in the VM build of k_walk
-    rt.walk_vm = q.g_in_walk || agg || q.nfa;
-    for (auto& it : q.select) rt.walk_vm |= it.src == SRC_VM;
+    rt.walk_vm = walk_vm;
     // closed-form fast path: `every A -> B` with f / g as term lists on the
     // events' own columns, plain-copy select items, <= 2 captures, <= 512
     // keys per bucket (CEP_NO_CF=1 forces the general path)

@@ -424,7 +424,7 @@ constexpr int kPartThreads = 512;
 constexpr int kPartItems = 4;             // tile = 2048 rows
 constexpr int kWalkThreads = 512;
 constexpr int kWalkWindow = 1024;         // records per LDS window
-constexpr int kWalkMaxTiles = 2048;       // tiles per chunk
+constexpr int kWalkMaxTiles = 8192;       // tiles per chunk (16 Mi rows)
 constexpr int kWalkMaxKeys = 512;         // keys per bucket (LDS histogram)
 constexpr int kWalkCapLds = 2;            // carried record words kept in LDS (closed form)
 constexpr int kMaxPending = 16;           // pending_slots upper bound (walk LDS lists)

@@ -893,9 +893,14 @@ namespace {
 constexpr int kEntryRec = 64;   // working-list ids >= 64 name window records
 constexpr int kWalkSlotStage = 2048;   // u64 words of staged per-key state (closed form)
 
+// Tiles per chunk the walk's segment tables hold: the VM build (sequences,
+// aggregates: one LDS-heavy workgroup per CU either way) takes 16 Mi-row
+// chunks so per-key state is loaded and committed once per 16 Mi events;
+// the 2-state build keeps 4 Mi-row chunks and two workgroups per CU.
+template <bool kVm>
+constexpr int walk_max_tiles() { return kVm ? kWalkMaxTiles : kWalkMaxTiles / 4; }
+
 struct WalkLds {
-  uint32_t seg[kWalkMaxTiles + 1];   // exclusive prefix of segment sizes
-  uint16_t lo[kWalkMaxTiles];        // segment start inside each tile
   uint32_t wrec[kWalkWindow];        // global record index per window slot
   uint16_t wkey[kWalkWindow];        // key within the bucket
   uint16_t sorted[kWalkWindow];      // window slots grouped by key, arrival order
@@ -1410,6 +1415,8 @@ template <bool kVm>
 __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
   __shared__ WalkLds L;
   __shared__ uint64_t R[kVm ? kMaxRegs * kWalkThreads : 1];   // VM registers, [reg][lane]
+  __shared__ uint32_t Lseg[walk_max_tiles<kVm>() + 1];        // exclusive prefix of segment sizes
+  __shared__ uint16_t Llo[walk_max_tiles<kVm>()];             // segment start inside each tile
   const int tid = threadIdx.x;
   const PatternArgs& p = a.pat;
   const int P = 1 << p.buckets_log2;
@@ -1433,17 +1440,18 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
 
   // segment starts and sizes -> exclusive prefix over tiles
   {
-    const int per = (ntiles + kWalkThreads - 1) / kWalkThreads;   // <= 4
-    uint32_t cnt[4];
+    constexpr int MAXPER = walk_max_tiles<kVm>() / kWalkThreads;   // 4 or 16
+    const int per = (ntiles + kWalkThreads - 1) / kWalkThreads;   // <= MAXPER
+    uint32_t cnt[MAXPER];
     uint32_t sum = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MAXPER; ++i) {
       const int t = tid * per + i;
       cnt[i] = 0;
       if (i < per && t < ntiles) {
         const uint16_t* o = a.tile_off + (int64_t)t * (P + 1) + bucket;
         const uint32_t lo = o[0], hi = o[1];
-        L.lo[t] = (uint16_t)lo;
+        Llo[t] = (uint16_t)lo;
         cnt[i] = hi - lo;
       }
       sum += cnt[i];
@@ -1451,14 +1459,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     uint32_t total;
     uint32_t off = block_excl_scan(sum, L.scratch, &total);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MAXPER; ++i) {
       const int t = tid * per + i;
       if (i < per && t < ntiles) {
-        L.seg[t] = off;
+        Lseg[t] = off;
         off += cnt[i];
       }
     }
-    if (tid == 0) L.seg[ntiles] = total;
+    if (tid == 0) Lseg[ntiles] = total;
   }
   lds_barrier();
   WALK_STAMP(1);
@@ -1469,10 +1477,10 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
       // largest t1 with seg[t1] - seg[t0] <= window (a single tile's segment is
       // at most tile_rows = 2048 > window: such a tile is split below)
       int lo = t0 + 1, hi = ntiles;
-      const uint32_t lim = L.seg[t0] + kWalkWindow;
+      const uint32_t lim = Lseg[t0] + kWalkWindow;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (L.seg[mid] <= lim) lo = mid;
+        if (Lseg[mid] <= lim) lo = mid;
         else hi = mid - 1;
       }
       L.t1 = (uint32_t)lo;
@@ -1480,8 +1488,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     for (int k = tid; k <= kpb; k += kWalkThreads) L.kstart[k] = 0;
     lds_barrier();
     const int t1 = (int)L.t1;
-    const uint32_t wbase = L.seg[t0];
-    const uint32_t nrec = L.seg[t1] - wbase;
+    const uint32_t wbase = Lseg[t0];
+    const uint32_t nrec = Lseg[t1] - wbase;
     if (nrec > kWalkWindow) {   // one tile holds more than a window of this bucket
       set_err(a.err, ERR_WINDOW);
     }
@@ -1489,8 +1497,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     // gather the window: record indices per tile segment (LDS only), then one
     // independent 16-byte header load (+ carried words) per record
     for (int t = t0 + tid; t < t1; t += kWalkThreads) {
-      const uint32_t pos = L.seg[t] - wbase, cnt = L.seg[t + 1] - L.seg[t];
-      const uint32_t g0 = (uint32_t)t * (uint32_t)a.tile_rows + L.lo[t];
+      const uint32_t pos = Lseg[t] - wbase, cnt = Lseg[t + 1] - Lseg[t];
+      const uint32_t g0 = (uint32_t)t * (uint32_t)a.tile_rows + Llo[t];
       for (uint32_t j = 0; j < cnt && pos + j < (uint32_t)kWalkWindow; ++j) L.wrec[pos + j] = g0 + j;
     }
     lds_barrier();

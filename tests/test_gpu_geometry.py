@@ -94,3 +94,26 @@ def test_config3_bench_geometry():
     m, dig, _ = CO.pattern_mt(w, K, F, G, True, 10000, threads=16)
     assert m == len(want["k"])
     assert workload.rows_digest(out["k"], out["p1"], out["p2"], out["t"], out["seq"]) == dig
+
+
+def test_vm_walk_16mi_chunks_vs_oracle():
+    # the interpreter build of the walk (computed select items, sequences,
+    # aggregates) takes 16 Mi-row chunks: a chunk spanning 8192 partition
+    # tiles, plus a short second one, vs the C oracle
+    import torch
+    plan = workload.PATTERN_PLAN.replace("s1.price as p1", "s1.price * 2.0 as p1")
+    n = (1 << 24) + 123457
+    rt = fs.SiddhiAppRuntime(plan, chunk_events=1 << 24, ordered_output=0)
+    d = workload.generate_device(0, n, K, rate=R)
+    rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
+    ts, seq, cols = rt.output_tensors("O")
+    rt.flush()
+    st = rt.stats()
+    assert st.kernel_launches[L.K_WALK] == 2 and st.kernel_launches[L.K_CF_WALK] == 0
+    got = {"k": cols[0].cpu().numpy(), "p1": cols[1].cpu().numpy() / 2.0, "p2": cols[2].cpu().numpy(),
+           "t": cols[3].cpu().numpy(), "ts": ts.cpu().numpy(), "seq": seq.cpu().numpy()}
+    rt.shutdown()
+    del d
+    torch.cuda.empty_cache()
+    w = CO.generate(0, n, K, rate=R, threads=16)
+    assert_same_per_key(got, oracle_rows(w, K))
