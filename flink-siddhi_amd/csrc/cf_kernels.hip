@@ -616,7 +616,7 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
 
 }  // namespace
 
-template <int NW, bool KR>
+template <int NW, bool KR, int NC>   // NC: captured words per pending slot (slot_words - 2)
 __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   // 2 workgroups per CU
   constexpr int NT = kCfWalkThreads, RW = 1 + NW, WIN = cf_window<NW>();
   constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   const int kpb = (int)((p.key_capacity + P - 1) >> lg);
   const int ntiles = a.ntiles;
   const int64_t ks = a.kstride;
-  const int sw = p.slot_words;   // 2 + ncap
+  constexpr int sw = 2 + NC;     // p.slot_words
   const int S = p.pending_slots;
   const int64_t W = p.within;
   CF_STAMP(0);
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   // dynamically indexed array lands in scratch).  Word 1 of a slot (the A's
   // arrival number) is not needed by the closed form and is neither read nor
   // written here; slots >= 2 stay in HBM.
-  const bool c1 = sw > 2, c2 = sw > 3;
+  constexpr bool c1 = NC > 0, c2 = NC > 1;
   uint64_t t0r = 0, t1r = 0, a0c0 = 0, a0c1 = 0, a1c0 = 0, a1c1 = 0;
   bool dirty = false;   // header / slots 0-1 changed: stored at kernel end
   if (n > 0) {
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   // Per window, a key lane copies its slots >= 2 (one batch of independent
   // loads, before any of the window's stores) to pcache: words pcb + (j - 2)
   // * cw + {0: ts, 1: capture 0, 2: capture 1} for j - 2 < cn.
-  const int cw = 1 + (c1 ? 1 : 0) + (c2 ? 1 : 0);
+  constexpr int cw = 1 + (c1 ? 1 : 0) + (c2 ? 1 : 0);
   int cn = 0;
   uint32_t pcb = 0;
   auto slot_word = [&](int j, int w) -> uint64_t {
@@ -1261,20 +1261,22 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
   }
 }
 
+template <int NW, bool KR>
+static void launch_cf_walk_nc(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
+  const dim3 g((unsigned)nbuckets), b(kCfWalkThreads);
+  switch (a.pat.slot_words - 2) {
+    case 0: hipLaunchKernelGGL((k_cfwalk<NW, KR, 0>), g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_cfwalk<NW, KR, 1>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_cfwalk<NW, KR, 2>), g, b, 0, s, a); break;
+  }
+}
+
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
+  const bool kr = a.key_rev != nullptr;
   switch (a.cf.nw) {
-    case 0:
-      if (a.key_rev) hipLaunchKernelGGL((k_cfwalk<0, true>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
-      else hipLaunchKernelGGL((k_cfwalk<0, false>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
-      break;
-    case 1:
-      if (a.key_rev) hipLaunchKernelGGL((k_cfwalk<1, true>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
-      else hipLaunchKernelGGL((k_cfwalk<1, false>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
-      break;
-    default:
-      if (a.key_rev) hipLaunchKernelGGL((k_cfwalk<2, true>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
-      else hipLaunchKernelGGL((k_cfwalk<2, false>), dim3((unsigned)nbuckets), dim3(kCfWalkThreads), 0, s, a);
-      break;
+    case 0: kr ? launch_cf_walk_nc<0, true>(a, nbuckets, s) : launch_cf_walk_nc<0, false>(a, nbuckets, s); break;
+    case 1: kr ? launch_cf_walk_nc<1, true>(a, nbuckets, s) : launch_cf_walk_nc<1, false>(a, nbuckets, s); break;
+    default: kr ? launch_cf_walk_nc<2, true>(a, nbuckets, s) : launch_cf_walk_nc<2, false>(a, nbuckets, s); break;
   }
 }
 
