@@ -86,13 +86,13 @@ __device__ __forceinline__ uint32_t bscan(uint32_t v, uint32_t* scratch, uint32_
 
 // Carried word of each row: slot sa on A rows (role_a bit set), sb otherwise;
 // both slots uniform.
-template <int E>
-__device__ __forceinline__ void pick_carried(const uint64_t (&pv)[kPref][E], int sa, int sb,
+template <int E, int Q = kPref>
+__device__ __forceinline__ void pick_carried(const uint64_t (&pv)[Q][E], int sa, int sb,
                                              uint32_t role_a, uint64_t (&out)[E]) {
-  take_slot<E>(pv, sa, out);
+  take_slot<E, Q>(pv, sa, out);
   if (sb != sa) {
 #pragma unroll
-    for (int q = 0; q < kPref; ++q) {
+    for (int q = 0; q < Q; ++q) {
       if (sb == q) {
         asm volatile("");
 #pragma unroll
@@ -105,10 +105,10 @@ __device__ __forceinline__ void pick_carried(const uint64_t (&pv)[kPref][E], int
 // Columns of a lane's E rows (row0 + 64 e) for the fast paths: event ts,
 // stream handle and every prefetched slot, all loads issued before any use;
 // unused slots and the ts alias issue none (uniform branches).
-template <int E>
+template <int E, int Q = kPref>
 __device__ __forceinline__ void cf_load_cols(const RowsArgs& rows, const PrefPlan& pref, int ts_slot,
                                              int64_t row0, uint32_t valid, uint64_t (&tsv)[E],
-                                             uint32_t (&sb)[E], uint64_t (&pv)[kPref][E]) {
+                                             uint32_t (&sb)[E], uint64_t (&pv)[Q][E]) {
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const bool ok = (valid >> e) & 1u;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void cf_load_cols(const RowsArgs& rows, const PrefPla
     sb[e] = (ok && rows.stream) ? (uint32_t)rows.stream[row0 + 64 * e] : (uint32_t)rows.input;
   }
 #pragma unroll
-  for (int q = 0; q < kPref; ++q) {
+  for (int q = 0; q < Q; ++q) {
     const int c = pref.col[q];
     const int ty = rows.cols.t[c];
     if (q < pref.n && q != ts_slot) {
@@ -142,7 +142,7 @@ __device__ __forceinline__ void cf_load_cols(const RowsArgs& rows, const PrefPla
     }
   }
 #pragma unroll
-  for (int q = 0; q < kPref; ++q)
+  for (int q = 0; q < Q; ++q)
     if (q == ts_slot) {
 #pragma unroll
       for (int e = 0; e < E; ++e) pv[q][e] = tsv[e];
@@ -157,7 +157,7 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 }  // namespace
 
 // ============================================================== k_cfpart ==
-template <int NW, bool FR>   // FR: rows are received shuffle records
+template <int NW, bool FR, int NP = kPref>   // FR: rows are received shuffle records; NP prefetched columns
 __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   for (int e = 0; e < E; ++e) valid |= (r0 + 64 * e < a.rows.n ? 1u : 0u) << e;
   uint32_t role_a = 0, role_b = 0;
   uint64_t tsv[E];
-  uint64_t pv[kPref][E];
+  uint64_t pv[NP][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) tsv[e] = 0;
   uint64_t fkey[E], fc0[E], fc1[E];   // key and carried words per row
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
   }
   if (!FR && valid) {
     uint32_t sb[E];
-    cf_load_cols<E>(a.rows, a.pref, a.ts_slot, row0, valid, tsv, sb, pv);
+    cf_load_cols<E, NP>(a.rows, a.pref, a.ts_slot, row0, valid, tsv, sb, pv);
     uint32_t is_a = 0, is_b = 0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -255,12 +255,12 @@ __global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void
       if (bad) set_err(a.err, ERR_ORDER);
     }
     const uint32_t all = (1u << E) - 1u;
-    if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
-    if (is_b) role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
+    if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E, NP>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
+    if (is_b) role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E, NP>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
     // key (the host puts the key column in slot 0) and carried words (A
     // rows: the A's columns, else the B's) picked now, so pv dies here
-    if (NW > 0) pick_carried<E>(pv, a.cf.a_slot[0], a.cf.b_slot[0], role_a, fc0);
-    if (NW > 1) pick_carried<E>(pv, a.cf.a_slot[1], a.cf.b_slot[1], role_a, fc1);
+    if (NW > 0) pick_carried<E, NP>(pv, a.cf.a_slot[0], a.cf.b_slot[0], role_a, fc0);
+    if (NW > 1) pick_carried<E, NP>(pv, a.cf.a_slot[1], a.cf.b_slot[1], role_a, fc1);
     if (a.pref.key_slot >= 0) {
 #pragma unroll
       for (int e = 0; e < E; ++e) fkey[e] = pv[0][e];
@@ -1254,10 +1254,18 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
     }
     return;
   }
-  switch (a.cf.nw) {
-    case 0: hipLaunchKernelGGL((k_cfpart<0, false>), g, b, dyn, s, a); break;
-    case 1: hipLaunchKernelGGL((k_cfpart<1, false>), g, b, dyn, s, a); break;
-    default: hipLaunchKernelGGL((k_cfpart<2, false>), g, b, dyn, s, a); break;
+  // the local-rows build holds only the prefetched columns the plan reads
+  const int np = a.pref.n <= 2 ? 2 : a.pref.n;
+  switch (a.cf.nw * 8 + np) {
+    case 0 * 8 + 2: hipLaunchKernelGGL((k_cfpart<0, false, 2>), g, b, dyn, s, a); break;
+    case 0 * 8 + 3: hipLaunchKernelGGL((k_cfpart<0, false, 3>), g, b, dyn, s, a); break;
+    case 0 * 8 + 4: hipLaunchKernelGGL((k_cfpart<0, false, 4>), g, b, dyn, s, a); break;
+    case 1 * 8 + 2: hipLaunchKernelGGL((k_cfpart<1, false, 2>), g, b, dyn, s, a); break;
+    case 1 * 8 + 3: hipLaunchKernelGGL((k_cfpart<1, false, 3>), g, b, dyn, s, a); break;
+    case 1 * 8 + 4: hipLaunchKernelGGL((k_cfpart<1, false, 4>), g, b, dyn, s, a); break;
+    case 2 * 8 + 2: hipLaunchKernelGGL((k_cfpart<2, false, 2>), g, b, dyn, s, a); break;
+    case 2 * 8 + 3: hipLaunchKernelGGL((k_cfpart<2, false, 3>), g, b, dyn, s, a); break;
+    default: hipLaunchKernelGGL((k_cfpart<2, false, 4>), g, b, dyn, s, a); break;
   }
 }
 

@@ -100,13 +100,13 @@ __device__ __forceinline__ void decode(const uint4 (&r)[E / 2], int type, uint64
 }
 
 // Value of prefetched slot `slot` (uniform) for row e.
-template <int N>
-__device__ __forceinline__ uint64_t pick(const uint64_t (&v)[kPref][N], int slot, int e) {
+template <int N, int Q = kPref>
+__device__ __forceinline__ uint64_t pick(const uint64_t (&v)[Q][N], int slot, int e) {
   // masked OR rather than selects: a select chain on slot == q gets rewritten
   // into a dynamically indexed (scratch) array access
   uint64_t x = 0;
 #pragma unroll
-  for (int q = 0; q < kPref; ++q) x |= v[q][e] & (0ull - (uint64_t)(slot == q));
+  for (int q = 0; q < Q; ++q) x |= v[q][e] & (0ull - (uint64_t)(slot == q));
   return x;
 }
 
@@ -114,12 +114,12 @@ __device__ __forceinline__ uint64_t pick(const uint64_t (&v)[kPref][N], int slot
 // so only the taken slot's copies execute.  A select chain or masked OR over
 // every slot costs kPref times the VALU per row; the empty asm keeps each
 // branch a branch (it is not if-converted into selects).
-template <int N>
-__device__ __forceinline__ void take_slot(const uint64_t (&v)[kPref][N], int slot, uint64_t (&out)[N]) {
+template <int N, int Q = kPref>
+__device__ __forceinline__ void take_slot(const uint64_t (&v)[Q][N], int slot, uint64_t (&out)[N]) {
 #pragma unroll
   for (int e = 0; e < N; ++e) out[e] = 0;
 #pragma unroll
-  for (int q = 0; q < kPref; ++q) {
+  for (int q = 0; q < Q; ++q) {
     if (slot == q) {
       asm volatile("");
 #pragma unroll
@@ -129,17 +129,17 @@ __device__ __forceinline__ void take_slot(const uint64_t (&v)[kPref][N], int slo
 }
 
 // Term-list predicate over prefetched rows (eval_terms_run without loads).
-template <int N>
+template <int N, int Q = kPref>
 __device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const int32_t* slot,
                                                     const ColSet& cols,
-                                                    const uint64_t (&vals)[kPref][N]) {
+                                                    const uint64_t (&vals)[Q][N]) {
   uint32_t acc = tl.any ? 0u : ((N >= 32) ? 0xffffffffu : ((1u << N) - 1u));
 #pragma unroll
   for (int i = 0; i < kMaxTerms; ++i) {   // fixed indices: term descriptors load once (SGPRs)
     if (i >= tl.n) break;
     const Term& t = tl.t[i];
     uint64_t v[N];
-    take_slot<N>(vals, slot[i], v);   // one uniform branch, not a masked OR over every slot
+    take_slot<N, Q>(vals, slot[i], v);   // one uniform branch, not a masked OR over every slot
     int ty = (t.coltype == T_BOOL || t.coltype == T_STRING) ? T_INT : t.coltype;
     uint32_t nullm = 0;
     if (t.aop) {
