@@ -1205,9 +1205,22 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   }
   // ---- hot-key candidates: keys that made this bucket long (hot.hip)
   if (klane && a.hot_thresh && kcnt > a.hot_thresh) {
-    const uint32_t i = atomicAdd(a.hot_ncand, 1u);
-    if (i < (uint32_t)kCfHotMax * 4)
-      a.hot_cand[i] = ((uint64_t)kcnt << 32) | (uint64_t)(uint32_t)(((int64_t)tid << lg) | bucket);
+    // two tiers, so the busiest keys are never crowded out by many merely
+    // warm ones: [0, kCfHotMax) for keys over 8x the threshold, the rest after
+    const uint32_t key = (uint32_t)(((int64_t)tid << lg) | bucket);
+    const uint64_t v = ((uint64_t)kcnt << 32) | key;
+    bool put = false;
+    if (kcnt >= 8u * a.hot_thresh) {
+      const uint32_t i = atomicAdd(&a.hot_ncand[0], 1u);
+      if (i < (uint32_t)kCfHotMax) {
+        a.hot_cand[i] = v;
+        put = true;
+      }
+    }
+    if (!put) {
+      const uint32_t j = atomicAdd(&a.hot_ncand[1], 1u);
+      if (j < 3u * kCfHotMax) a.hot_cand[kCfHotMax + j] = v;
+    }
   }
   // ---- an overflow run still in the read pool moves to the write pool
   // (the read pool is the next launch's write pool)

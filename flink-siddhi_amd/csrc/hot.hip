@@ -608,32 +608,42 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
 __global__ __launch_bounds__(kCfHotMax) void k_hot_update(HotArgs a, int diverted) {
   constexpr int NC = kCfHotMax * 4;
   __shared__ uint64_t c[NC];
+  __shared__ uint64_t sm[kCfHotMax];     // slots by records (ascending): m << 32 | slot
   __shared__ uint32_t freel[kCfHotMax];
   __shared__ uint32_t scan[kCfHotMax];
-  __shared__ uint32_t nfree;
+  __shared__ uint32_t nfree, nrest;
   const int h = threadIdx.x;
+  auto block_incl_scan = [&](uint32_t v) -> uint32_t {   // inclusive scan over the block
+    scan[h] = v;
+    __syncthreads();
+    for (int d = 1; d < kCfHotMax; d <<= 1) {
+      const uint32_t x = h >= d ? scan[h - d] : 0u;
+      __syncthreads();
+      scan[h] += x;
+      __syncthreads();
+    }
+    const uint32_t r = scan[h];
+    __syncthreads();
+    return r;
+  };
   if (diverted && a.hot_key[h] >= 0 && a.hot_m[h] < a.thresh / 4) {
     a.hot_id[a.hot_key[h]] = kNotHot;
     a.hot_key[h] = -1;
   }
-  const uint32_t nc = min(*a.ncand, a.cand_cap);
+  const uint32_t n0 = min(a.ncand[0], (uint32_t)kCfHotMax);
+  const uint32_t n1 = min(a.ncand[1], 3u * kCfHotMax);
+  const uint32_t nc = n0 + n1;
   __syncthreads();
   if (nc > 0) {
     uint32_t N = 2;
     while (N < nc) N <<= 1;
-    for (uint32_t i = h; i < N; i += kCfHotMax) c[i] = i < nc ? a.cand[i] : 0ull;
+    for (uint32_t i = h; i < N; i += kCfHotMax)
+      c[i] = i < n0 ? a.cand[i] : (i < nc ? a.cand[kCfHotMax + (i - n0)] : 0ull);
     // free slots, in slot order
     const uint32_t f = a.hot_key[h] < 0 ? 1u : 0u;
-    scan[h] = f;
-    __syncthreads();
-    for (int d = 1; d < kCfHotMax; d <<= 1) {
-      const uint32_t v = h >= d ? scan[h - d] : 0u;
-      __syncthreads();
-      scan[h] += v;
-      __syncthreads();
-    }
-    if (f) freel[scan[h] - 1] = (uint32_t)h;
-    if (h == kCfHotMax - 1) nfree = scan[h];
+    const uint32_t fs = block_incl_scan(f);
+    if (f) freel[fs - 1] = (uint32_t)h;
+    if (h == kCfHotMax - 1) nfree = fs;
     __syncthreads();
     // candidates, busiest first (bitonic sort, descending)
     for (uint32_t k = 2; k <= N; k <<= 1) {
@@ -652,40 +662,83 @@ __global__ __launch_bounds__(kCfHotMax) void k_hot_update(HotArgs a, int diverte
         __syncthreads();
       }
     }
-    // the first nfree candidates that are not hot yet take the free slots
-    // (a key appears once: one walk lane per key)
+    // the busiest candidates not hot yet take the free slots (one walk lane
+    // per key: no key appears twice)
     for (uint32_t i0 = 0; i0 < nc; i0 += kCfHotMax) {
       const uint32_t i = i0 + h;
       const uint32_t k = i < nc ? (uint32_t)c[i] : 0u;
       const uint32_t adm = (i < nc && a.hot_id[k] == kNotHot) ? 1u : 0u;
-      scan[h] = adm;
-      __syncthreads();
-      for (int d = 1; d < kCfHotMax; d <<= 1) {
-        const uint32_t v = h >= d ? scan[h - d] : 0u;
-        __syncthreads();
-        scan[h] += v;
-        __syncthreads();
-      }
-      const uint32_t rank = scan[h] - adm;
+      const uint32_t rank = block_incl_scan(adm) - adm;
       const uint32_t nf = nfree;
       if (adm && rank < nf) {
         const uint32_t slot = freel[rank];
         a.hot_key[slot] = (int32_t)k;
         a.hot_id[k] = (uint16_t)slot;
         a.hot_m[slot] = a.thresh;   // not evicted before it has been measured
+        c[i] = 0;                   // taken
       }
       __syncthreads();
       if (h == kCfHotMax - 1) {
-        const uint32_t used = min(scan[h], nf);
+        const uint32_t used = min(scan[h] + 0u, nf);   // scan[] holds the round's inclusive total
         nfree = nf - used;
         for (uint32_t x = 0; x < nf - used; ++x) freel[x] = freel[x + used];
       }
       __syncthreads();
       if (nfree == 0) break;
     }
+    // all slots taken: a candidate far busier than a slot's key this chunk
+    // replaces it (pairs the i-th busiest waiting candidate with the i-th
+    // idlest slot), so the hot set converges on the busiest keys
+    if (diverted) {
+      // waiting candidates, compacted in order
+      uint32_t w = 0;
+      for (uint32_t i0 = 0; i0 < nc; i0 += kCfHotMax) {
+        const uint32_t i = i0 + h;
+        const uint32_t k = i < nc ? (uint32_t)c[i] : 0u;
+        const uint32_t wt = (i < nc && c[i] != 0 && a.hot_id[k] == kNotHot) ? 1u : 0u;
+        const uint32_t r = block_incl_scan(wt) - wt;
+        const uint64_t v = i < nc ? c[i] : 0ull;
+        __syncthreads();
+        if (wt && w + r < (uint32_t)kCfHotMax) c[w + r] = v;   // (in place: w + r <= i)
+        w += scan[kCfHotMax - 1];
+        __syncthreads();
+      }
+      if (h == 0) nrest = min(w, (uint32_t)kCfHotMax);
+      const int32_t hk = a.hot_key[h];
+      sm[h] = hk >= 0 ? (((uint64_t)a.hot_m[h] << 32) | (uint32_t)h) : ~0ull;
+      __syncthreads();
+      for (int k = 2; k <= kCfHotMax; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const int ixj = h ^ j;
+          if (ixj > h) {
+            const uint64_t x = sm[h], y = sm[ixj];
+            const bool asc = (h & k) == 0;
+            if ((x > y) == asc) {
+              sm[h] = y;
+              sm[ixj] = x;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      if ((uint32_t)h < nrest && sm[h] != ~0ull) {
+        const uint64_t cand = c[h];
+        const uint32_t cm = (uint32_t)(cand >> 32), k = (uint32_t)cand;
+        const uint32_t sm_m = (uint32_t)(sm[h] >> 32), slot = (uint32_t)sm[h];
+        if ((uint64_t)cm > 4ull * sm_m) {
+          a.hot_id[a.hot_key[slot]] = kNotHot;
+          a.hot_key[slot] = (int32_t)k;
+          a.hot_id[k] = (uint16_t)slot;
+          a.hot_m[slot] = a.thresh;
+        }
+      }
+    }
   }
   __syncthreads();
-  if (h == 0) *a.ncand = 0;
+  if (h == 0) {
+    a.ncand[0] = 0;
+    a.ncand[1] = 0;
+  }
   // slots in use
   scan[h] = a.hot_key[h] >= 0 ? 1u : 0u;
   __syncthreads();

@@ -167,3 +167,21 @@ def test_hot_keys_on_shuffle_owners(world):
             "ts": w["ts"][b], "seq": b}
     assert hot > 0, "hot-key path never engaged on the owners"
     assert_same_per_key(got, want)
+
+
+def test_low_threshold_fills_every_slot(monkeypatch):
+    # threshold 16 at 1 Mi-event chunks: thousands of candidates per chunk, so
+    # the candidate tiers overflow, all 1024 slots fill and busier keys
+    # replace idle hot keys (k_hot_update's replacement pass); keys change hands
+    # between the walk and the hot scans every chunk
+    monkeypatch.setenv("CEP_HOT_THRESH", "16")
+    keys, rate, n = 1 << 16, 400, 1 << 21
+    za = workload.zipf_map(keys, seed=21)
+    zb = workload.zipf_map(keys, seed=22)
+    tables = [za, za, zb, zb, za]
+    batches = [(i * n, n, t) for i, t in enumerate(tables)]
+    got, st = run_batches(batches, keys, rate, workload.PATTERN_PLAN, 1 << 20)
+    want, _ = oracle_batches(batches, keys, rate, CO.cond(("id", 7, "==", 0)), 10000)
+    assert st.kernel_launches[L.K_HOT] > 0
+    assert st.hot_keys > 512, st.hot_keys
+    assert_same_per_key(got, want)
