@@ -41,7 +41,9 @@ constexpr int kCfStageBytes = (kCfTile / 8192 * 20 + 36) * 1024;    // a tile ke
 
 // Block-wide exclusive scan of one value per thread, NT <= 1024 threads;
 // scratch holds NT / 64 + 1 words.
-template <int NT>
+// kTail = false: no trailing barrier; the caller must not write `scratch`
+// again before another barrier (the walk alternates two scratch buffers).
+template <int NT, bool kTail = true>
 __device__ __forceinline__ uint32_t bscan(uint32_t v, uint32_t* scratch, uint32_t* total) {
   constexpr int NWV = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -66,7 +68,7 @@ __device__ __forceinline__ uint32_t bscan(uint32_t v, uint32_t* scratch, uint32_
   lds_barrier();
   const uint32_t r = scratch[wave] + x - v;
   *total = scratch[NWV];
-  lds_barrier();
+  if (kTail) lds_barrier();
   return r;
 }
 
@@ -557,8 +559,11 @@ constexpr int cf_window() { return NW > 1 ? 1536 : kCfWindow; }
 template <int NW, int WIN = cf_window<NW>()>
 struct CfWalkLds {
   uint32_t seg[kCfMaxTiles + 1];       // exclusive prefix of the bucket's segment sizes
-  uint32_t kstart[kCfMaxKeys + 1];     // key runs (sorted positions)
-  uint32_t kcur[kCfMaxKeys];           // counting-sort cursors
+  uint32_t kstart[2][kCfMaxKeys + 1];  // key runs (sorted positions); alternating windows
+  union {
+    uint32_t kcur[kCfMaxKeys];         // counting-sort cursors (p3)
+    uint32_t klast[kCfMaxKeys];        // ts of the run's last A (if khasa; p4 - p6)
+  };
   union {
     uint32_t wrec[WIN];                // arena record index per window slot (gather, reload)
     uint64_t pcache[WIN / 2];          // from p4: key lanes' pending slots >= 2 (ts, captures)
@@ -578,12 +583,12 @@ struct CfWalkLds {
   uint16_t v[WIN];                     // output row offset per sorted position
   uint16_t kfb[kCfMaxKeys];            // first B of the key's run, or kNoB
   uint16_t klb[kCfMaxKeys];            // last B of the key's run, or kNoB
-  uint32_t klast[kCfMaxKeys];          // ts of the run's last A (if khasa)
   uint8_t khasa[kCfMaxKeys];
   uint8_t cm[kCfMaxKeys];              // carried partials completed by the key's first B
   uint32_t obits[kCfTile / 32];        // oversize segment: tile-row presence bitmap
   uint16_t opre[kCfTile / 32];         // oversize segment: popcount prefix per bitmap word
   uint32_t scratch[kCfWalkThreads / 64 + 1];
+  uint32_t scratch2[kCfWalkThreads / 64 + 1];   // the output scan's (no tail barrier)
   unsigned long long base;
 };
 
@@ -737,7 +742,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
   };
   const int64_t ts_base = a.chunk_base[0];
   const int64_t seq_base = a.chunk_base[1];
-  for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
+  int kbuf = 0;   // this window's key-run buffer
+  for (int k = tid; k <= kpb; k += NT) L.kstart[0][k] = 0;
 
   // ---- segment sizes -> exclusive prefix over tiles; this thread's segment
   // starts stay in registers (lop) for the gather
@@ -862,21 +868,21 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       const uint64_t h = ((uint64_t)x[i].y << 32) | x[i].x;
       hk[i] = rec_key(h);
       hs[i] = (L.wrec[q < nw ? q : 0] & ~(uint32_t)(kCfTile - 1)) + rec_row(h);
-      if (q < nw) atomicAdd(&L.kstart[hk[i] + 1], 1u);
+      if (q < nw) atomicAdd(&L.kstart[kbuf][hk[i] + 1], 1u);
     }
     lds_barrier();
     CF_STAMP(wi * 8 + 2);
     // ---- counting sort by key of (seq, key, slot) entries, then each entry's
     // arrival rank inside its key run -> sorted position of window slot q
     {
-      const uint32_t c = tid < kpb ? L.kstart[tid + 1] : 0u;
+      const uint32_t c = tid < kpb ? L.kstart[kbuf][tid + 1] : 0u;
       uint32_t total;
-      const uint32_t off = bscan<NT>(c, L.scratch, &total);
+      const uint32_t off = bscan<NT, false>(c, L.scratch, &total);
       if (tid < kpb) {
-        L.kstart[tid] = off;
+        L.kstart[kbuf][tid] = off;
         L.kcur[tid] = off;
       }
-      if (tid == 0) L.kstart[kpb] = total;
+      if (tid == 0) L.kstart[kbuf][kpb] = total;
     }
     lds_barrier();
 #pragma unroll
@@ -893,7 +899,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       if (s >= nw) continue;
       const uint64_t e = L.kent[s];
       const uint32_t k = (uint32_t)(e >> 11) & 0x1ffu;
-      const uint32_t r0 = L.kstart[k], r1 = L.kstart[k + 1];
+      const uint32_t r0 = L.kstart[kbuf][k], r1 = L.kstart[kbuf][k + 1];
       uint32_t rank = 0;
       for (uint32_t j = r0; j < r1; ++j) rank += (L.kent[j] >> 20) < (e >> 20) ? 1u : 0u;
       L.sorted[e & 0x7ffu] = (uint16_t)(r0 + rank);
@@ -926,7 +932,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     uint64_t pv0[2], pv1[2], pv2[2];
     uint32_t pco = 0;
     const int ni = min(n, S);   // inline slots in use (overflow slots are read from the pool)
-    const bool fill = klane && ni > 2 && L.kstart[tid + 1] > L.kstart[tid];
+    const bool fill = klane && ni > 2 && L.kstart[kbuf][tid + 1] > L.kstart[kbuf][tid];
     if (fill) {
       const uint32_t need = (uint32_t)((ni - 2) * cw);
       pco = atomicAdd(&L.pc_used, need);
@@ -950,7 +956,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       if (s >= nw) continue;
       const uint32_t kr = L.skr[s];
       const uint32_t k = kr & 0xfffu, role = kr >> 12;
-      const uint32_t r1 = L.kstart[k + 1];
+      const uint32_t r1 = L.kstart[kbuf][k + 1];
       uint16_t nb = kNoB;
       bool later_a = false;
       for (uint32_t j = s + 1; j < r1; ++j) {
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         L.khasa[k] = 1;
       }
       if ((role & ROLE_B) && nb == kNoB) L.klb[k] = (uint16_t)s;
-      if (s == L.kstart[k]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)s : nb;
+      if (s == L.kstart[kbuf][k]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)s : nb;
     }
     if (cn > 0) {
       auto put_pc = [&](int j, uint64_t t, uint64_t x0, uint64_t x1) {
@@ -988,8 +994,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     int cfirst = 0, cm = 0;
     uint64_t e00 = 0, e01 = 0, e10 = 0, e11 = 0;
     if (klane) {
-      r0 = L.kstart[tid];
-      r1 = L.kstart[tid + 1];
+      r0 = L.kstart[kbuf][tid];
+      r1 = L.kstart[kbuf][tid + 1];
       kcnt += r1 - r0;
       const uint16_t fb = L.kfb[tid];
       if (r1 > r0 && fb != kNoB && n > 0) {
@@ -1035,13 +1041,13 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
             const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
             val = (W < 0 || (d < 0 ? -d : d) <= W) ? 1u : 0u;
           }
-          if (q == L.kstart[k]) val += L.cm[k];
+          if (q == L.kstart[kbuf][k]) val += L.cm[k];
         }
         vals[i] = val;
         sum += val;
       }
       uint32_t total;
-      uint32_t off = bscan<NT>(sum, L.scratch, &total);
+      uint32_t off = bscan<NT, false>(sum, L.scratch2, &total);
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         L.v[tid * PER + i] = (uint16_t)off;
@@ -1174,7 +1180,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
       if (W >= 0 && (d < 0 ? -d : d) > W) continue;
       const uint32_t k = kr & 0xfffu;
-      const uint32_t extra = q == L.kstart[k] ? L.cm[k] : 0u;
+      const uint32_t extra = q == L.kstart[kbuf][k] ? L.cm[k] : 0u;
       const int64_t ats = ts_base + (int64_t)L.sts[q];
       const int64_t bts = ts_base + (int64_t)L.sts[nb];
       const uint64_t a0 = NW > 0 ? L.scap[0][q] : 0ull, a1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][q] : 0ull;
@@ -1198,10 +1204,12 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     if (!over && (t0 >= ntiles || L.seg[t0] >= nall)) break;
     wi = 1;
     // next window: the LDS arrays are reused (a key's slots >= 2 are read
-    // back only by the lane that wrote them)
+    // back only by the lane that wrote them).  Its key-run buffer is the one
+    // the previous window used, read by nobody since: zeroed without a
+    // second barrier (its counts are added after the next window's first)
     lds_barrier();
-    for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
-    lds_barrier();
+    kbuf ^= 1;
+    for (int k = tid; k <= kpb; k += NT) L.kstart[kbuf][k] = 0;
   }
   // ---- hot-key candidates: keys that made this bucket long (hot.hip)
   if (klane && a.hot_thresh && kcnt > a.hot_thresh) {
