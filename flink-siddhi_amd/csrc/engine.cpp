@@ -140,6 +140,7 @@ struct PatternRT {
   // (sticky) once the device has put a key into a hot slot
   bool hot = false;            // candidate collection on (closed-form path, P + kCfHotMax buckets fit)
   bool hot_on = false;         // diversion active: hot arenas allocated
+  bool hot_probed = false;     // the first (short) chunk ran and its candidates were read back
   uint32_t hot_thresh = 0;     // records per key per launch that make a key hot
   int hot_blocks = 0;
   DevBuf hot_id, hot_key, hot_m, hot_gbase, hoff, cand, ncand, harr, hrow, hnb, bsum, bcnt, boff, hcm, hobase,
@@ -689,12 +690,21 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     hipEventRecord(a->in_ready, a->stream);
     hipStreamWaitEvent(a->side, a->in_ready, 0);
   }
-  for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.cf_chunk) {
+  // Hot-key probe: until diversion has been decided once, the first chunk is
+  // short (kHotProbeRows) and followed by one stream sync, so a skewed
+  // stream's hottest keys are diverted from the second chunk on instead of
+  // one workgroup walking a hot key's whole run of a full chunk (seconds at
+  // Zipf s = 1.1).  Uniform streams pay one short chunk and one sync per
+  // runtime.
+  constexpr int64_t kHotProbeRows = 1 << 20;
+  for (int64_t r0 = 0, step = 0; r0 < rows_all.n; r0 += step) {
     const int b = rt.cur;
     rt.cur ^= 1;
+    const bool probe = rt.hot && !rt.hot_on && !rt.hot_probed;
+    step = std::min<int64_t>(probe ? std::min<int64_t>(kHotProbeRows, rt.cf_chunk) : rt.cf_chunk, rows_all.n - r0);
     RowsArgs rows = rows_all;
     rows.row0 = rows_all.row0 + r0;
-    rows.n = std::min<int64_t>(rt.cf_chunk, rows_all.n - r0);
+    rows.n = step;
     if (r0 > 0) rows.prev_ts = INT64_MIN;   // checked inside the kernel via ts[row-1]
     const int64_t ntiles = (rows.n + kCfTile - 1) / kCfTile;
     CfPartArgs pa{};
@@ -843,6 +853,10 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       if (divert && !hot_serial) hipStreamWaitEvent(a->stream, rt.hot_join, 0);
       launch_hot_update(ha, divert ? 1 : 0, a->stream);
       hipMemcpyAsync(rt.hot_active_host.p, rt.hot_active.p, 4, hipMemcpyDeviceToHost, a->stream);
+      if (probe) {   // the probe's verdict decides the next chunk's diversion
+        hipStreamSynchronize(a->stream);
+        rt.hot_probed = true;
+      }
     }
     rt.pool_side ^= 1;   // this launch's write pool holds every run now
     if (overlap) hipEventRecord(rt.walk_done[b], a->stream);
