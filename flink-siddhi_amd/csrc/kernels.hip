@@ -145,7 +145,7 @@ __device__ __forceinline__ uint32_t eval_run(const TermList& tl, const VmArgs& v
 // kVm = false: filter and projection are TermList / direct copies (no interpreter).
 template <bool kVm>
 __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
-  constexpr int kStageWords = 4096;   // plain-copy output stage (32 KiB)
+  constexpr int kStageWords = 16 * kFilterThreads;   // plain-copy output stage (16 words per lane)
   __shared__ uint64_t R[kVm ? kMaxRegs * kFilterThreads : kStageWords];
   __shared__ uint32_t scratch[16];
   __shared__ uint32_t s_tile;
@@ -180,40 +180,54 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
   const uint32_t mine = (uint32_t)__popc(sel);
   const uint32_t off = block_excl_scan(mine, scratch, &total);
 
-  if (tid == 0) {
+  // Decoupled look-back, one wave wide: lane l reads the flag of tile
+  // (base - l); the nearest inclusive prefix among the 64 ends the walk once
+  // every nearer predecessor has published its aggregate, otherwise all 64
+  // aggregates are added and the window moves 64 tiles back.
+  if (tid < 64) {
+    const int lane = tid;
     unsigned long long* flags = a.tile_state;
     unsigned long long prefix = 0;
     if (tile == 0) {
       prefix = __hip_atomic_load(a.out.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      __hip_atomic_store(&flags[tile], (1ull << kStatusShift) | total, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      int64_t j = tile - 1;
-      while (j >= 0) {
-        unsigned long long v;
-        unsigned spins = 0;
-        do {
-          v = __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((v >> kStatusShift) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            ++spins;
+      if (lane == 0)
+        __hip_atomic_store(&flags[tile], (1ull << kStatusShift) | total, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      int64_t base = tile - 1;
+      unsigned spins = 0;
+      while (true) {
+        const int64_t j = base - lane;
+        const unsigned long long v =
+            j >= 0 ? __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const uint32_t st = (uint32_t)(v >> kStatusShift);
+        const uint64_t ready = __ballot(st != 0);
+        const uint64_t incl = __ballot(st == 2);
+        const int f = incl ? __ffsll((long long)incl) - 1 : 63;
+        const uint64_t need = f == 63 ? ~0ull : ((2ull << f) - 1ull);   // lanes 0..f
+        if ((ready & need) != need) {   // a nearer predecessor has not published yet
+          if (++spins > (1u << 22)) {   // never published: give up loudly
+            if (lane == 0) set_err(a.err, ERR_WINDOW);
+            break;
           }
-        } while ((v >> kStatusShift) == 0 && spins < (1u << 22));
-        if ((v >> kStatusShift) == 0) {   // predecessor never published: give up loudly
-          set_err(a.err, ERR_WINDOW);
-          break;
+          __builtin_amdgcn_s_sleep(1);
+          continue;
         }
-        prefix += v & kValueMask;
-        if ((v >> kStatusShift) == 2) break;
-        --j;
+        unsigned long long x = ((need >> lane) & 1ull) ? (v & kValueMask) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        prefix += x;
+        if (incl) break;
+        base -= 64;
       }
     }
-    __hip_atomic_store(&flags[tile], (2ull << kStatusShift) | (prefix + total),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_prefix = prefix;
-    if (tile == (int64_t)gridDim.x - 1)
-      __hip_atomic_store(a.out.count, prefix + total, __ATOMIC_RELAXED,
+    if (lane == 0) {
+      __hip_atomic_store(&flags[tile], (2ull << kStatusShift) | (prefix + total), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = prefix;
+      if (tile == (int64_t)gridDim.x - 1)
+        __hip_atomic_store(a.out.count, prefix + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   int64_t pos = (int64_t)s_prefix + off;

@@ -111,6 +111,34 @@ def test_config2_filter_parity():
     assert abs(len(want) / 200000 - 0.08) < 0.01
 
 
+def test_config2_filter_many_tiles_vs_c_oracle():
+    """3 * 2^20 events in three batches: ~130 tiles of 8192 rows per batch,
+    so the look-back walks past its 64-tile window; every selected row (its
+    columns, ts and arrival number, in order) vs oracle/cep_oracle.c."""
+    import cep_oracle as CO
+    n, batches = 3 << 20, 3
+    w = workload.generate(0, n, 1 << 20, single_stream=True)
+    rt = fs.SiddhiAppRuntime(workload.FILTER_PLAN)
+    rt.add_callback("O")
+    name = rt.intern("test_event")
+    names = np.full(n, name, np.int32)
+    cuts = np.linspace(0, n, batches + 1).astype(int)
+    for b in range(batches):
+        s, e = cuts[b], cuts[b + 1]
+        rt.send("inputStream", w["ts"][s:e], [w["id"][s:e], names[s:e], w["price"][s:e], w["ts"][s:e]])
+    rt.flush()
+    out = rt.collect("O")
+    rt.shutdown()
+    sel = CO.filter_indices(w["id"], w["price"], CO.cond(("price", 0, ">", 0.5), ("id", 7, "==", 0)))
+    assert len(sel) > 0.07 * n
+    np.testing.assert_array_equal(out.seq, sel)
+    np.testing.assert_array_equal(out.ts, w["ts"][sel])
+    np.testing.assert_array_equal(out.cols[0], w["id"][sel])
+    np.testing.assert_array_equal(out.cols[1], names[sel])
+    np.testing.assert_array_equal(out.cols[2], w["price"][sel])
+    np.testing.assert_array_equal(out.cols[3], w["ts"][sel])
+
+
 def test_filter_expression_semantics():
     plan = ("define stream S (a int, b long, c float, d double, e bool);"
             "from S[(a % 3 == -1 or a / 4 > 2) and not e or d / 0.0 > 1.0e300] "
