@@ -420,7 +420,7 @@ void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
 
 // 512 lanes x 16 rows: 8192-row tiles halve the decoupled look-back chains
 // of 4096-row tiles (config 2: 907 -> 830 us per 10^8 events)
-constexpr int kFilterThreads = 512;
+constexpr int kFilterThreads = 512;   // 1024 lanes (16384-row tiles): 878 us
 constexpr int kFilterItems = 16;          // rows per thread per tile
 constexpr int kPartThreads = 512;
 constexpr int kPartItems = 4;             // tile = 2048 rows

@@ -178,7 +178,28 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
   }
   uint32_t total;
   const uint32_t mine = (uint32_t)__popc(sel);
-  const uint32_t off = block_excl_scan(mine, scratch, &total);
+  uint32_t off;
+  {   // block exclusive scan (up to 16 waves)
+    const int lane = tid & 63, wave = tid >> 6;
+    constexpr int NWV = kFilterThreads / 64;
+    uint32_t x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) scratch[wave] = x;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const uint32_t c = scratch[w];
+      wb += w < wave ? c : 0u;
+      tot += c;
+    }
+    off = wb + x - mine;
+    total = tot;
+  }
 
   // Decoupled look-back, one wave wide: lane l reads the flag of tile
   // (base - l); the nearest inclusive prefix among the 64 ends the walk once
