@@ -201,6 +201,31 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
     total = tot;
   }
 
+  // Plain-copy projection (kVm = false): the tile's selected rows are staged
+  // in LDS column by column, then each column's run [prefix, prefix + total)
+  // is written with consecutive lanes on consecutive rows.  The in-tile
+  // offsets are known before the tile's prefix, so the staging loads are
+  // issued before the look-back (wave 0 looks back first, the other waves
+  // stage meanwhile).  A tile selecting more rows than the stage holds, or
+  // one that would pass the output capacity, stores directly.
+  const int nc = a.out.ncols;
+  const uint32_t cap = (uint32_t)(kStageWords / (nc + 2));
+  const bool stage = !kVm && total <= cap;   // uniform
+  auto stage_rows = [&]() {
+    uint32_t slot = off;
+    for (uint32_t m = sel; m; m &= m - 1) {
+      const int64_t row = row0 + (__ffs(m) - 1);
+      for (int c = 0; c < nc; ++c) {
+        const int col = a.out.src[c] - SRC_REC;
+        R[c * cap + slot] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], row);
+      }
+      R[nc * cap + slot] = (uint64_t)a.rows.ts[row];
+      R[(nc + 1) * cap + slot] = (uint64_t)row_seq(a.rows, row);
+      ++slot;
+    }
+  };
+  if (stage && tid >= 64) stage_rows();
+
   // Decoupled look-back, one wave wide: lane l reads the flag of tile
   // (base - l); the nearest inclusive prefix among the 64 ends the walk once
   // every nearer predecessor has published its aggregate, otherwise all 64
@@ -250,42 +275,19 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
         __hip_atomic_store(a.out.count, prefix + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (stage && tid < 64) stage_rows();
   __syncthreads();
   int64_t pos = (int64_t)s_prefix + off;
-  if constexpr (!kVm) {
-    // Plain-copy projection: stage the tile's selected rows in LDS column by
-    // column, then write each column's run [prefix, prefix +
-    // total) with consecutive lanes on consecutive rows — one contiguous
-    // store stream per column instead of one scattered store per row and
-    // column.  A tile selecting more rows than the stage holds, or one that
-    // would pass the output capacity, stores directly.
-    const int nc = a.out.ncols;
-    const uint32_t cap = (uint32_t)(kStageWords / (nc + 2));
+  if (stage && (int64_t)s_prefix + (int64_t)total <= a.out.cap) {   // uniform
     const int64_t prefix = (int64_t)s_prefix;
-    if (total <= cap && prefix + (int64_t)total <= a.out.cap) {   // uniform
-      uint32_t slot = off;
-      while (sel) {
-        const int e = __ffs(sel) - 1;
-        sel &= sel - 1;
-        const int64_t row = row0 + e;
-        for (int c = 0; c < nc; ++c) {
-          const int col = a.out.src[c] - SRC_REC;
-          R[c * cap + slot] = load_col(a.rows.cols.p[col], a.rows.cols.t[col], row);
-        }
-        R[nc * cap + slot] = (uint64_t)a.rows.ts[row];
-        R[(nc + 1) * cap + slot] = (uint64_t)row_seq(a.rows, row);
-        ++slot;
-      }
-      __syncthreads();
-      for (int c = 0; c < nc; ++c)
-        for (uint32_t j = tid; j < total; j += kFilterThreads)
-          store_col(a.out.col[c], a.out.type[c], prefix + j, R[c * cap + j]);
-      for (uint32_t j = tid; j < total; j += kFilterThreads) {
-        a.out.ts[prefix + j] = (int64_t)R[nc * cap + j];
-        a.out.seq[prefix + j] = (int64_t)R[(nc + 1) * cap + j];
-      }
-      return;
+    for (int c = 0; c < nc; ++c)
+      for (uint32_t j = tid; j < total; j += kFilterThreads)
+        store_col(a.out.col[c], a.out.type[c], prefix + j, R[c * cap + j]);
+    for (uint32_t j = tid; j < total; j += kFilterThreads) {
+      a.out.ts[prefix + j] = (int64_t)R[nc * cap + j];
+      a.out.seq[prefix + j] = (int64_t)R[(nc + 1) * cap + j];
     }
+    return;
   }
   while (sel) {
     const int e = __ffs(sel) - 1;
