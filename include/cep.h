@@ -23,6 +23,11 @@
  * for the engine.  Output rows handed to the callback are owned by the engine
  * and valid only during the callback.  Snapshot buffers are engine-allocated
  * and released with cep_free().
+ *
+ * Hot-key probe: a keyed `every A -> B` runtime on the closed-form path
+ * walks its first 2^20 rows as a short chunk and waits for it once inside
+ * that cep_send_batch() (its hot-key verdict decides the next chunk's
+ * routing); every later call returns without a sync.
  */
 #ifndef CEP_H_
 #define CEP_H_
