@@ -51,6 +51,39 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratc
   return r;
 }
 
+// Block-wide exclusive scan of one value per thread, NT <= 1024 threads;
+// scratch holds NT / 64 + 1 words.
+// kTail = false: no trailing barrier; the caller must not write `scratch`
+// again before another barrier (the walk alternates two scratch buffers).
+template <int NT, bool kTail = true>
+__device__ __forceinline__ uint32_t bscan(uint32_t v, uint32_t* scratch, uint32_t* total) {
+  constexpr int NWV = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) scratch[wave + 1] = x;
+  lds_barrier();
+  if (wave == 0) {
+    uint32_t s = (lane < NWV) ? scratch[lane + 1] : 0u;
+#pragma unroll
+    for (int o = 1; o < NWV; o <<= 1) {
+      const uint32_t y = __shfl_up(s, o, 64);
+      if (lane >= o) s += y;
+    }
+    if (lane < NWV) scratch[lane + 1] = s;   // inclusive prefix of wave totals
+    if (lane == 0) scratch[0] = 0;
+  }
+  lds_barrier();
+  const uint32_t r = scratch[wave] + x - v;
+  *total = scratch[NWV];
+  if (kTail) lds_barrier();
+  return r;
+}
+
 // Shard-local dense key of partition key `key` (cep_options key_stride /
 // key_offset: this shard owns key % stride == offset), or -1 when the key is
 // negative or not owned.  stride == 1 (one shard) skips the division; else a
@@ -152,6 +185,53 @@ __device__ __forceinline__ uint32_t eval_terms_regs(const TermList& tl, const in
     acc = tl.any ? (acc | bits) : (acc & bits);
   }
   return acc;
+}
+
+// Columns of a lane's E rows (row0 + 64 e) for the fast paths: event ts,
+// stream handle and every prefetched slot, all loads issued before any use;
+// unused slots and the ts alias issue none (uniform branches).
+template <int E, int Q = kPref>
+__device__ __forceinline__ void cf_load_cols(const RowsArgs& rows, const PrefPlan& pref, int ts_slot,
+                                             int64_t row0, uint32_t valid, uint64_t (&tsv)[E],
+                                             uint32_t (&sb)[E], uint64_t (&pv)[Q][E]) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const bool ok = (valid >> e) & 1u;
+    tsv[e] = ok ? (uint64_t)rows.ts[row0 + 64 * e] : 0ull;
+    sb[e] = (ok && rows.stream) ? (uint32_t)rows.stream[row0 + 64 * e] : (uint32_t)rows.input;
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = pref.col[q];
+    const int ty = rows.cols.t[c];
+    if (q < pref.n && q != ts_slot) {
+      const void* base = rows.cols.p[c];
+      if (ty == T_LONG || ty == T_DOUBLE) {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          pv[q][e] = ((valid >> e) & 1u) ? ((const uint64_t*)base)[row0 + 64 * e] : 0ull;
+      } else if (ty == T_BOOL) {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          pv[q][e] = ((valid >> e) & 1u) ? (((const uint8_t*)base)[row0 + 64 * e] ? 1ull : 0ull) : 0ull;
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const uint32_t v = ((valid >> e) & 1u) ? ((const uint32_t*)base)[row0 + 64 * e] : 0u;
+          pv[q][e] = ty == T_FLOAT ? (uint64_t)v : from_i32((int32_t)v);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) pv[q][e] = 0;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (q == ts_slot) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) pv[q][e] = tsv[e];
+    }
 }
 
 // XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md

@@ -149,6 +149,32 @@ struct PatternRT {
   hipEvent_t hot_fork = nullptr, hot_join = nullptr;   // hot kernels on the side stream, beside the walk
 };
 
+// Multi-query group (mq_kernels.hip): keyed queries of one app sharing a
+// key column, run by one partition pass + one walk per chunk.
+struct MqRT {
+  std::vector<int> qs;                   // query indices, plan order
+  std::vector<MqQuery> hq;               // host copy of the device descriptors
+  DevBuf dq, dconds;
+  std::vector<MqCond> conds;             // [8][kMqMaxCond]
+  int32_t ncond[8] = {0};
+  uint32_t stream_mask = 0;
+  int key_col = -1;
+  std::vector<int> carry;                // logical carried columns
+  std::vector<int> cond_cols;            // columns the conditions read
+  bool check_order = false;
+  int64_t key_capacity = 0, kstride = 0;
+  int lg = 0, kpb = 0;
+  int key_stride = 1, key_offset = 0;
+  DevBuf state;
+  int64_t words = 0;                     // state words per key (all queries)
+  int64_t chunk = 0;
+  DevBuf recs[2], toff[2], chunk_base[2];
+  hipEvent_t part_done[2] = {nullptr, nullptr}, walk_done[2] = {nullptr, nullptr};
+  bool used[2] = {false, false};
+  int cur = 0;
+  bool dq_dirty = true;
+};
+
 struct TimedLaunch {
   int kind;
   hipEvent_t a, b;
@@ -175,6 +201,8 @@ struct cep_app {
   DevBuf code, konst;
   std::vector<OutStream> outs;
   std::vector<PatternRT> pats;
+  std::vector<MqRT> mqs;          // multi-query groups
+  std::vector<char> in_mq;        // per query: served by a multi-query group
   DevBuf tile_state, ticket, err;
   DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
@@ -303,6 +331,317 @@ OutArgs out_args(OutStream& o, const Query& q) {
   return oa;
 }
 
+// ---- multi-query groups (mq_kernels.hip) ------------------------------------
+// A query joins a group when its per-event work is interpreter-free and keyed
+// on the group's key column: group-by aggregations (term-list filter, plain
+// column arguments, select items key / aggregate / column, having on one
+// output item) and sequences of the one-live-partial shape (a single start
+// event on a stream no later state reads) with own-column term-list
+// conditions and first / last captures.  Queries of one group share the
+// partition pass (one read of the batch, each distinct condition evaluated
+// once per row) and the walk (AbstractSiddhiOperator.java:283-287: every
+// event goes to every query).  CEP_NO_MQ=1: no groups (general path).
+bool same_layout(const CompiledApp& app, int s, int t) {
+  const auto& x = app.inputs[s].attrs;
+  const auto& y = app.inputs[t].attrs;
+  if (x.size() != y.size()) return false;
+  for (size_t c = 0; c < x.size(); ++c)
+    if (x[c].type != y[c].type) return false;
+  return true;
+}
+
+bool same_terms(const TermList& x, const TermList& y) {
+  if (x.n != y.n || x.any != y.any) return false;
+  for (int i = 0; i < x.n; ++i) {
+    const Term &u = x.t[i], &v = y.t[i];
+    if (u.col != v.col || u.coltype != v.coltype || u.aop != v.aop || u.atype != v.atype || u.aconst != v.aconst ||
+        u.cop != v.cop || u.ctype != v.ctype || u.cconst != v.cconst)
+      return false;
+  }
+  return true;
+}
+
+// What one query adds to a group: its conditions per stream, carried columns.
+struct MqNeeds {
+  int key_col = -1, layout = -1;
+  std::vector<std::pair<int, TermList>> conds;   // (stream, condition), n == 0: always true
+  std::vector<int> carry;                        // columns carried in records
+  std::vector<int> cols;                         // columns conditions read
+};
+
+bool mq_candidate(const cep_app* a, const Query& q, MqNeeds* nd) {
+  const CompiledApp& app = a->app;
+  if (a->opt.sparse_keys) return false;
+  auto key_ok = [&](int s, int col) {
+    if (s < 0 || col < 0) return false;
+    const int t = app.inputs[s].attrs[col].type;
+    return t == T_INT || t == T_LONG;
+  };
+  auto add_cols = [&](const TermList& tl) {
+    for (int i = 0; i < tl.n; ++i)
+      if (std::find(nd->cols.begin(), nd->cols.end(), tl.t[i].col) == nd->cols.end()) nd->cols.push_back(tl.t[i].col);
+  };
+  auto carry = [&](int col) {
+    if (col == nd->key_col) return;
+    if (std::find(nd->carry.begin(), nd->carry.end(), col) == nd->carry.end()) nd->carry.push_back(col);
+  };
+  if (q.kind == Q_AGG) {
+    if (q.in_stream < 0 || !key_ok(q.in_stream, q.key_col)) return false;
+    if ((int)q.aggs.size() > kMqMaxAggs || !q.having_simple || (int)q.select.size() > kMqMaxSel) return false;
+    if (q.f.valid() && q.f_terms.n < 0) return false;
+    nd->key_col = q.key_col;
+    nd->layout = q.in_stream;
+    TermList f;
+    f.n = 0;
+    if (q.f.valid()) f = q.f_terms;
+    nd->conds.push_back({q.in_stream, f});
+    add_cols(f);
+    for (auto& ag : q.aggs) {
+      if (ag.arg.valid() && ag.word < 0) return false;
+      if (ag.word >= 0) carry(q.rec_cols_a[ag.word]);
+    }
+    for (auto& it : q.select) {
+      if (it.src == SRC_KEY || (it.src >= SRC_AGG && it.src < SRC_AGG + (int)q.aggs.size())) continue;
+      if (it.src >= SRC_REC && it.src < SRC_REC + (int)q.rec_cols_a.size()) {
+        carry(q.rec_cols_a[it.src - SRC_REC]);
+        continue;
+      }
+      return false;
+    }
+    return true;
+  }
+  if (q.kind != Q_PATTERN || !q.nfa || !q.sequence) return false;
+  const int n = (int)q.nstates.size();
+  if (n < 1 || n > kMaxStates || q.nstates[0].min_count != 1 || q.nstates[0].max_count != 1) return false;
+  if ((int)q.ncaps.size() > kMqMaxCaps || (int)q.select.size() > kMqMaxSel) return false;
+  for (int j = 0; j < n; ++j) {
+    const auto& st = q.nstates[j];
+    if (j > 0 && st.stream == q.nstates[0].stream) return false;   // one live partial per key
+    if (st.walk.valid() || st.terms.n < 0 || st.min_count > 254 || st.max_count > 254) return false;
+    const int col = st.stream < (int)q.key_col_s.size() ? q.key_col_s[st.stream] : -1;
+    if (!key_ok(st.stream, col) || (nd->key_col >= 0 && col != nd->key_col)) return false;
+    if (!same_layout(app, st.stream, q.nstates[0].stream)) return false;
+    nd->key_col = col;
+  }
+  nd->layout = q.nstates[0].stream;
+  for (int j = 0; j < n; ++j) {
+    nd->conds.push_back({q.nstates[j].stream, q.nstates[j].terms});
+    add_cols(q.nstates[j].terms);
+  }
+  for (auto& cp : q.ncaps) {
+    if (cp.index != 0 && cp.index != -1) return false;
+    carry(q.rec_cols_a[cp.word]);
+  }
+  for (auto& it : q.select)
+    if (!(it.src == SRC_KEY || (it.src >= SRC_CAP && it.src < SRC_CAP + (int)q.ncaps.size()))) return false;
+  return true;
+}
+
+int mq_index(std::vector<int>& v, int x) {
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i] == x) return (int)i;
+  v.push_back(x);
+  return (int)v.size() - 1;
+}
+
+// Condition bit of `tl` on stream s in group g (added when new); -1: full.
+int mq_cond_bit(MqRT& g, int s, const TermList& tl, bool add) {
+  if (tl.n == 0) return kMqTrueBit;
+  for (int c = 0; c < g.ncond[s]; ++c)
+    if (same_terms(g.conds[s * kMqMaxCond + c].tl, tl)) return c;
+  if (g.ncond[s] >= kMqMaxCond) return -1;
+  if (!add) return g.ncond[s];
+  MqCond& mc = g.conds[s * kMqMaxCond + g.ncond[s]];
+  std::memset(&mc, 0, sizeof(mc));
+  mc.tl = tl;
+  return g.ncond[s]++;
+}
+
+// Prefetched columns of a group: the key first, then condition and carried
+// columns (k_mqpart loads each once per row).
+std::vector<int> mq_pref_cols(const MqRT& g) {
+  std::vector<int> v{g.key_col};
+  for (int c : g.cond_cols) mq_index(v, c);
+  for (int c : g.carry) mq_index(v, c);
+  return v;
+}
+
+int build_mq_groups(cep_app* a) {
+  const CompiledApp& app = a->app;
+  a->in_mq.assign(app.queries.size(), 0);
+  if (std::getenv("CEP_NO_MQ") || app.inputs.size() > 8) return CEP_OK;
+  std::vector<int> layouts;   // per group: a stream of its layout
+  for (size_t qi = 0; qi < app.queries.size(); ++qi) {
+    MqNeeds nd;
+    if (!mq_candidate(a, app.queries[qi], &nd)) continue;
+    int gi = -1;
+    for (size_t i = 0; i < a->mqs.size() && gi < 0; ++i) {
+      MqRT& g = a->mqs[i];
+      if ((int)g.qs.size() >= kMqMaxQ || g.key_col != nd.key_col || !same_layout(app, layouts[i], nd.layout))
+        continue;
+      // conditions, carried and prefetched columns still fit
+      int extra[8] = {0};
+      bool ok = true;
+      for (auto& c : nd.conds) {
+        const int b = mq_cond_bit(g, c.first, c.second, false);
+        if (b < 0) ok = false;
+        else if (b == g.ncond[c.first]) {
+          bool dup = false;   // the same new condition twice in this query
+          for (auto& d : nd.conds)
+            if (&d != &c && d.first == c.first && same_terms(d.second, c.second) && &d < &c) dup = true;
+          if (!dup) ++extra[c.first];
+        }
+      }
+      for (int s = 0; s < 8 && ok; ++s) ok = g.ncond[s] + extra[s] <= kMqMaxCond;
+      MqRT t;
+      t.key_col = g.key_col;
+      t.cond_cols = g.cond_cols;
+      t.carry = g.carry;
+      for (int c : nd.cols) mq_index(t.cond_cols, c);
+      for (int c : nd.carry) mq_index(t.carry, c);
+      ok = ok && (int)t.carry.size() <= kMqMaxCarry && (int)mq_pref_cols(t).size() <= kPref;
+      if (ok) gi = (int)i;
+    }
+    if (gi < 0) {
+      MqRT g;
+      g.key_col = nd.key_col;
+      g.conds.resize(8 * kMqMaxCond);
+      for (int c : nd.cols) mq_index(g.cond_cols, c);
+      for (int c : nd.carry) mq_index(g.carry, c);
+      if ((int)g.carry.size() > kMqMaxCarry || (int)mq_pref_cols(g).size() > kPref) continue;
+      int per[8] = {0};
+      for (auto& c : nd.conds) per[c.first]++;
+      bool ok = true;
+      for (int s = 0; s < 8; ++s) ok = ok && per[s] <= kMqMaxCond;
+      if (!ok) continue;
+      a->mqs.push_back(std::move(g));
+      layouts.push_back(nd.layout);
+      gi = (int)a->mqs.size() - 1;
+    }
+    MqRT& g = a->mqs[gi];
+    for (int c : nd.cols) mq_index(g.cond_cols, c);
+    for (int c : nd.carry) mq_index(g.carry, c);
+    for (auto& c : nd.conds) mq_cond_bit(g, c.first, c.second, true);
+    g.qs.push_back((int)qi);
+    a->in_mq[qi] = 1;
+  }
+  // device descriptors, state and arenas per group
+  for (auto& g : a->mqs) {
+    const int64_t K = a->opt.key_capacity;
+    g.key_capacity = K;
+    g.key_stride = std::max(1, a->opt.key_stride);
+    g.key_offset = a->opt.key_offset;
+    int64_t chunk = std::max<int64_t>(a->opt.chunk_events, kMqTile);
+    chunk = std::min<int64_t>(chunk, (int64_t)kMqMaxTiles * kMqTile);
+    g.chunk = (chunk / kMqTile) * kMqTile;
+    const int nphys_max = std::min<int>((int)g.carry.size(), kMqMaxPhys);
+    const int W = nphys_max <= 1 ? kMqWindow : (nphys_max == 2 ? 3072 : 2048);
+    // keys per bucket: about half a window of records per bucket per chunk
+    int64_t kpb = 64;
+    while (kpb * 2 <= kMqMaxKpb && (double)g.chunk * (double)(kpb * 2) / (double)K <= W / 2) kpb *= 2;
+    int lg = 0;
+    while (((K + (1 << lg) - 1) >> lg) > kpb) ++lg;
+    while (lg > 0 && (1 << lg) > kMqMaxBuckets) --lg;
+    kpb = (K + (1 << lg) - 1) >> lg;
+    if (kpb > kMqMaxKpb) return fail(a, CEP_E_CAPACITY, "key_capacity too large for a multi-query group");
+    g.lg = lg;
+    g.kpb = (int)kpb;
+    g.kstride = kpb << lg;
+    // descriptors
+    int64_t off = 0;
+    for (int qi : g.qs) {
+      const Query& q = app.queries[qi];
+      MqQuery d;
+      std::memset(&d, 0, sizeof(d));
+      d.st_off = off;
+      const int oi = app.output_index(q.out_stream);
+      const auto& od = app.outputs[oi];
+      d.nsel = (int)q.select.size();
+      for (int i = 0; i < d.nsel; ++i) d.sel_type[i] = od.attrs[i].type;
+      d.hav_item = -1;
+      auto lword = [&](int col) { return col == g.key_col ? (int)MQ_SRC_KEY : mq_index(g.carry, col); };
+      if (q.kind == Q_AGG) {
+        d.kind = MQ_AGG;
+        d.in_stream = q.in_stream;
+        d.stream_mask = 1u << q.in_stream;
+        TermList f;
+        f.n = 0;
+        if (q.f.valid()) f = q.f_terms;
+        d.filter_bit = mq_cond_bit(g, q.in_stream, f, false);
+        d.nagg = (int)q.aggs.size();
+        for (int i = 0; i < d.nagg; ++i) {
+          d.agg_fn[i] = q.aggs[i].fn;
+          d.agg_arg_type[i] = q.aggs[i].arg_type;
+          d.agg_out_type[i] = q.aggs[i].out_type;
+          d.agg_src[i] = q.aggs[i].word >= 0 ? lword(q.rec_cols_a[q.aggs[i].word]) : (int)MQ_SRC_KEY;
+        }
+        for (int i = 0; i < d.nsel; ++i) {
+          const int src = q.select[i].src;
+          d.sel_src[i] = (src >= SRC_REC && src < SRC_REC + (int)q.rec_cols_a.size())
+                             ? SRC_REC + lword(q.rec_cols_a[src - SRC_REC])
+                             : src;
+        }
+        if (q.having_item >= 0) {
+          d.hav_item = q.having_item;
+          d.hav_cop = q.having_cop;
+          d.hav_ctype = q.having_ctype;
+          d.hav_cconst = q.having_cconst;
+        }
+        d.nwords = 1 + d.nagg;
+      } else {
+        d.kind = MQ_SEQ;
+        d.nstates = (int)q.nstates.size();
+        d.every = q.every ? 1 : 0;
+        d.within = q.within;
+        for (int j = 0; j < d.nstates; ++j) {
+          const auto& st = q.nstates[j];
+          d.stream_mask |= 1u << st.stream;
+          d.st_stream |= (uint32_t)st.stream << (3 * j);
+          d.st_bit |= (uint64_t)mq_cond_bit(g, st.stream, st.terms, false) << (6 * j);
+          d.st_min |= (uint64_t)st.min_count << (8 * j);
+          d.st_max |= (uint64_t)(st.max_count < 0 ? 0xff : st.max_count) << (8 * j);
+          bool opt = true;
+          for (int k = j + 1; k < d.nstates; ++k) opt = opt && q.nstates[k].min_count == 0;
+          if (opt) d.tail_opt |= 1u << j;
+        }
+        d.ncap = (int)q.ncaps.size();
+        for (int i = 0; i < d.ncap; ++i) {
+          d.cap_state[i] = q.ncaps[i].state;
+          d.cap_last[i] = q.ncaps[i].index < 0 ? 1 : 0;
+          d.cap_src[i] = lword(q.rec_cols_a[q.ncaps[i].word]);
+        }
+        for (int i = 0; i < d.nsel; ++i) d.sel_src[i] = q.select[i].src;
+        d.nwords = 2 + d.ncap;
+      }
+      g.stream_mask |= d.stream_mask;
+      g.check_order = g.check_order || (d.kind == MQ_SEQ && d.within >= 0);
+      off += d.nwords;
+      g.hq.push_back(d);
+    }
+    g.words = off;
+    const int ntiles = (int)(g.chunk / kMqTile);
+    bool ok = dev_ensure(&g.dq, g.hq.size() * sizeof(MqQuery), a->stream, false) &&
+              dev_ensure(&g.dconds, g.conds.size() * sizeof(MqCond), a->stream, false) &&
+              dev_ensure(&g.state, (size_t)g.words * g.kstride * 8, a->stream, false);
+    for (int b = 0; b < 2 && ok; ++b)
+      ok = dev_ensure(&g.recs[b], (size_t)g.chunk * (2 + nphys_max) * 8 + 16, a->stream, false) &&
+           dev_ensure(&g.toff[b], (size_t)((1 << lg) + 1) * ntiles * 2 + 16, a->stream, false) &&
+           dev_ensure(&g.chunk_base[b], 64, a->stream, false) &&
+           hipEventCreateWithFlags(&g.part_done[b], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&g.walk_done[b], hipEventDisableTiming) == hipSuccess;
+    if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (multi-query group)");
+    hipMemset(g.state.p, 0, (size_t)g.words * g.kstride * 8);
+    // condition slots: the prefetch slot of each term's column
+    const std::vector<int> pc = mq_pref_cols(g);
+    for (auto& mc : g.conds)
+      for (int i = 0; i < mc.tl.n && i < kMaxTerms; ++i)
+        for (size_t sl = 0; sl < pc.size(); ++sl)
+          if (pc[sl] == mc.tl.t[i].col) mc.slot[i] = (int32_t)sl;
+    hipMemcpy(g.dconds.p, g.conds.data(), g.conds.size() * sizeof(MqCond), hipMemcpyHostToDevice);
+  }
+  return CEP_OK;
+}
+
 int create_runtime(cep_app* a) {
   const CompiledApp& app = a->app;
   if (hipSetDevice(a->opt.device) != hipSuccess)
@@ -342,9 +681,14 @@ int create_runtime(cep_app* a) {
     hipMemset(o.count, 0, sizeof(unsigned long long));
     a->outs.push_back(std::move(o));
   }
+  {
+    const int rc = build_mq_groups(a);
+    if (rc) return rc;
+  }
   for (size_t qi = 0; qi < app.queries.size(); ++qi) {
     const Query& q = app.queries[qi];
     if (q.kind != Q_PATTERN && q.kind != Q_AGG) continue;
+    if (a->in_mq[qi]) continue;   // served by a multi-query group
     const bool agg = q.kind == Q_AGG;
     // group-by state: one slot of (accumulator, count) pairs per group
     const int S = agg ? 1 : a->opt.pending_slots;
@@ -985,9 +1329,129 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
   return CEP_OK;
 }
 
+// One batch through a multi-query group: per chunk, k_mqpart on the side
+// stream (double-buffered arenas: the partition of chunk c+1 overlaps the
+// walk of chunk c) and k_mqwalk on the main stream.
+int run_mq(cep_app* a, MqRT& g, const RowsArgs& rows_all) {
+  const CompiledApp& app = a->app;
+  // output capacity: at most one row per query per input row
+  for (size_t i = 0; i < g.qs.size(); ++i) {
+    const Query& q = app.queries[g.qs[i]];
+    OutStream& o = a->outs[app.output_index(q.out_stream)];
+    o.bound += rows_all.n;
+    const int rc = ensure_out_cap(a, o, o.bound);
+    if (rc) return rc;
+    MqQuery& d = g.hq[i];
+    bool same = d.out_ts == (int64_t*)o.ts.p && d.out_seq == (int64_t*)o.seq.p && d.out_count == o.count &&
+                d.out_cap == o.cap;
+    for (int c = 0; c < d.nsel; ++c) same = same && d.out_col[c] == o.cols[c].p;
+    if (!same) {
+      for (int c = 0; c < d.nsel; ++c) d.out_col[c] = o.cols[c].p;
+      d.out_ts = (int64_t*)o.ts.p;
+      d.out_seq = (int64_t*)o.seq.p;
+      d.out_count = o.count;
+      d.out_cap = o.cap;
+      g.dq_dirty = true;
+    }
+  }
+  if (g.dq_dirty) {   // rare (output growth): the walks in flight read the old table
+    hipStreamSynchronize(a->stream);
+    hipMemcpy(g.dq.p, g.hq.data(), g.hq.size() * sizeof(MqQuery), hipMemcpyHostToDevice);
+    g.dq_dirty = false;
+  }
+  // this batch's column layout: a carried column whose buffer IS the event-ts
+  // buffer is not carried (its value is the record's ts)
+  const std::vector<int> pc = mq_pref_cols(g);
+  MqPartArgs pa{};
+  pa.pref.n = (int)pc.size();
+  for (int i = 0; i < kPref; ++i) pa.pref.col[i] = i < pa.pref.n ? pc[i] : pc[0];
+  pa.ts_slot = -1;
+  for (int i = 0; i < pa.pref.n; ++i)
+    if (rows_all.cols.p[pc[i]] == (const void*)rows_all.ts && rows_all.cols.t[pc[i]] == T_LONG) pa.ts_slot = i;
+  MqWalkArgs wa{};
+  int nphys = 0;
+  for (size_t w = 0; w < g.carry.size(); ++w) {
+    const int col = g.carry[w];
+    if (rows_all.cols.p[col] == (const void*)rows_all.ts && rows_all.cols.t[col] == T_LONG) {
+      wa.lmap[w] = -1;
+      continue;
+    }
+    if (nphys >= kMqMaxPhys)
+      return fail(a, CEP_E_UNSUPPORTED, "multi-query group carries more than " + std::to_string(kMqMaxPhys) + " columns");
+    wa.lmap[w] = nphys;
+    for (int i = 0; i < pa.pref.n; ++i)
+      if (pc[i] == col) pa.phys_slot[nphys] = i;
+    ++nphys;
+  }
+  if (nphys > std::min<int>((int)g.carry.size(), kMqMaxPhys)) return fail(a, CEP_E_DEVICE, "record arena too small");
+  pa.stream_mask = g.stream_mask;
+  pa.key_slot = 0;
+  for (int s = 0; s < 8; ++s) pa.ncond[s] = g.ncond[s];
+  pa.conds = (const MqCond*)g.dconds.p;
+  pa.nphys = nphys;
+  pa.check_order = g.check_order ? 1 : 0;
+  pa.key_capacity = g.key_capacity;
+  pa.key_stride = g.key_stride;
+  pa.key_offset = g.key_offset;
+  pa.buckets_log2 = g.lg;
+  pa.err = (unsigned int*)a->err.p;
+  wa.q = (const MqQuery*)g.dq.p;
+  wa.nq = (int)g.qs.size();
+  wa.nphys = nphys;
+  wa.buckets_log2 = g.lg;
+  wa.kpb = g.kpb;
+  wa.key_stride = g.key_stride;
+  wa.key_offset = g.key_offset;
+  wa.state = (uint64_t*)g.state.p;
+  wa.kstride = g.kstride;
+  wa.err = pa.err;
+  // the side stream starts after everything already queued on the main one
+  hipEventRecord(a->in_ready, a->stream);
+  hipStreamWaitEvent(a->side, a->in_ready, 0);
+  static const bool no_overlap = std::getenv("CEP_NO_OVERLAP") != nullptr;
+  hipStream_t side = no_overlap ? a->stream : a->side;
+  for (int64_t r0 = 0; r0 < rows_all.n; r0 += g.chunk) {
+    const int b = g.cur;
+    g.cur ^= 1;
+    RowsArgs rows = rows_all;
+    rows.row0 = rows_all.row0 + r0;
+    rows.n = std::min<int64_t>(g.chunk, rows_all.n - r0);
+    const int ntiles = (int)((rows.n + kMqTile - 1) / kMqTile);
+    pa.rows = rows;
+    pa.ntiles = ntiles;
+    pa.chunk_base = (int64_t*)g.chunk_base[b].p;
+    pa.recs = (uint64_t*)g.recs[b].p;
+    pa.tile_off = (uint16_t*)g.toff[b].p;
+    if (g.used[b]) hipStreamWaitEvent(side, g.walk_done[b], 0);   // arena b is free
+    {
+      LaunchTimer t(a, CEP_K_MQ_PARTITION, side);
+      launch_mq_partition(pa, side);
+    }
+    hipEventRecord(g.part_done[b], side);
+    hipStreamWaitEvent(a->stream, g.part_done[b], 0);
+    wa.recs = pa.recs;
+    wa.tile_off = pa.tile_off;
+    wa.ntiles = ntiles;
+    wa.chunk_base = pa.chunk_base;
+    wa.in_seq = rows.seq ? rows.seq + rows.row0 : nullptr;
+    {
+      LaunchTimer t(a, CEP_K_MQ_WALK);
+      launch_mq_walk(wa, 1 << g.lg, a->stream);
+    }
+    hipEventRecord(g.walk_done[b], a->stream);
+    g.used[b] = true;
+  }
+  return CEP_OK;
+}
+
 int send_device_rows(cep_app* a, const RowsArgs& rows) {
+  for (auto& g : a->mqs) {
+    const int rc = run_mq(a, g, rows);
+    if (rc) return rc;
+  }
   for (size_t qi = 0; qi < a->app.queries.size(); ++qi) {
     const Query& q = a->app.queries[qi];
+    if (a->in_mq[qi]) continue;
     int rc = CEP_OK;
     if (q.kind == Q_FILTER) {
       rc = run_filter(a, q, rows);
@@ -1221,6 +1685,14 @@ void cep_destroy(cep_app* a) {
       dev_free(&p.chunk_base[b]);
     }
   }
+  for (auto& g : a->mqs) {
+    for (DevBuf* b : {&g.dq, &g.dconds, &g.state}) dev_free(b);
+    for (int b = 0; b < 2; ++b) {
+      dev_free(&g.recs[b]);
+      dev_free(&g.toff[b]);
+      dev_free(&g.chunk_base[b]);
+    }
+  }
   if (a->copy) hipStreamSynchronize(a->copy);
   for (auto& h : a->hs) {
     host_free(&h.pinned);
@@ -1261,6 +1733,11 @@ void cep_destroy(cep_app* a) {
     for (int b = 0; b < 2; ++b) {
       if (p.part_done[b]) hipEventDestroy(p.part_done[b]);
       if (p.walk_done[b]) hipEventDestroy(p.walk_done[b]);
+    }
+  for (auto& g : a->mqs)
+    for (int b = 0; b < 2; ++b) {
+      if (g.part_done[b]) hipEventDestroy(g.part_done[b]);
+      if (g.walk_done[b]) hipEventDestroy(g.walk_done[b]);
     }
   if (a->in_ready) hipEventDestroy(a->in_ready);
   if (a->ext_ready) hipEventDestroy(a->ext_ready);
@@ -1725,7 +2202,10 @@ void cep_free(void* p) { std::free(p); }
 //   definition (type width each), n x i64 ts, n x u8 stream if has_stream;
 //   (version 4) per pattern: u8 sparse keys, if set u32 count, u32 id of
 //   the value -1 (0xffffffff: none), count x i64 partition value per dense slot.
-// Versions 2 (no reorder section) and 3 are still restored.
+//   (version 5) u32 n_groups, per multi-query group: i64 key_capacity,
+//   u32 words per key, u32 n_live, n_live x { u32 key, words x u64 }.
+// Versions 2 (no reorder section), 3 and 4 are still restored (apps without
+// multi-query groups).
 static uint64_t plan_hash(const CompiledApp& app) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](const void* p, size_t n) {
@@ -1747,7 +2227,7 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
   };
   const char magic[4] = {'C', 'E', 'P', 'S'};
   put(magic, 4);
-  uint32_t ver = 4;   // 3: + the event-time reorder buffer; 4: + pending counts (overflow runs)
+  uint32_t ver = 5;   // 3: + the event-time reorder buffer; 4: + pending counts (overflow runs); 5: + groups
   put(&ver, 4);
   uint64_t h = plan_hash(a->app);
   put(&h, 8);
@@ -1826,6 +2306,33 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
     if (cnt[0]) hipMemcpy(rev.data(), rt.krev.p, rev.size() * 8, hipMemcpyDeviceToHost);
     put(rev.data(), rev.size() * 8);
   }
+  // (version 5) multi-query groups: per group every key whose state is not
+  // all zero, with the group's state words (query by query, plan order)
+  {
+    const uint32_t ng = (uint32_t)a->mqs.size();
+    put(&ng, 4);
+    for (auto& g : a->mqs) {
+      const int64_t ks = g.kstride, kpb = g.kpb;
+      const uint32_t nw = (uint32_t)g.words;
+      std::vector<uint64_t> st((size_t)g.words * ks);
+      hipMemcpy(st.data(), g.state.p, st.size() * 8, hipMemcpyDeviceToHost);
+      std::vector<uint32_t> live;
+      for (int64_t i = 0; i < ks; ++i) {
+        bool any = false;
+        for (uint32_t w = 0; w < nw && !any; ++w) any = st[(size_t)w * ks + i] != 0;
+        if (any) live.push_back((uint32_t)i);
+      }
+      const uint32_t nl = (uint32_t)live.size();
+      put(&g.key_capacity, 8);
+      put(&nw, 4);
+      put(&nl, 4);
+      for (uint32_t i : live) {
+        const uint32_t key = (uint32_t)(((i % kpb) << g.lg) | (i / kpb));   // dense key
+        put(&key, 4);
+        for (uint32_t w = 0; w < nw; ++w) put(&st[(size_t)w * ks + i], 8);
+      }
+    }
+  }
   *buf = (uint8_t*)std::malloc(out.size());
   if (!*buf) return fail(a, CEP_E_DEVICE, "out of host memory");
   std::memcpy(*buf, out.data(), out.size());
@@ -1847,7 +2354,7 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
   uint64_t h;
   int64_t ev;
   uint32_t np;
-  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver < 2 || ver > 4 || !get(&h, 8) ||
+  if (!get(magic, 4) || std::memcmp(magic, "CEPS", 4) || !get(&ver, 4) || ver < 2 || ver > 5 || !get(&h, 8) ||
       !get(&ev, 8) || !get(&np, 4))
     return fail(a, CEP_E_STATE, "not a libcep snapshot");
   if (h != plan_hash(a->app) || np != a->pats.size())
@@ -1964,6 +2471,31 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     for (auto& rt : a->pats)
       if (rt.sparse) return fail(a, CEP_E_STATE, "snapshot has no key map (version < 4)");
   }
+  // (version 5) multi-query group state
+  std::vector<std::vector<uint64_t>> mst(a->mqs.size());
+  if (ver >= 5) {
+    uint32_t ng;
+    if (!get(&ng, 4) || ng != a->mqs.size()) return fail(a, CEP_E_STATE, "snapshot multi-query groups do not match");
+    for (size_t gi = 0; gi < a->mqs.size(); ++gi) {
+      const MqRT& g = a->mqs[gi];
+      int64_t kc;
+      uint32_t nw, nl;
+      if (!get(&kc, 8) || !get(&nw, 4) || !get(&nl, 4)) return fail(a, CEP_E_STATE, "truncated snapshot");
+      if (kc != g.key_capacity || nw != (uint32_t)g.words || nl > (uint64_t)kc)
+        return fail(a, CEP_E_STATE, "snapshot geometry differs from this runtime");
+      if ((uint64_t)nl * (4 + 8ull * nw) > len - off) return fail(a, CEP_E_STATE, "truncated snapshot");
+      mst[gi].assign((size_t)g.words * g.kstride, 0);
+      for (uint32_t i = 0; i < nl; ++i) {
+        uint32_t key;
+        get(&key, 4);
+        if (key >= kc) return fail(a, CEP_E_STATE, "corrupt snapshot");
+        const int64_t idx = (int64_t)(key & ((1u << g.lg) - 1)) * g.kpb + (key >> g.lg);
+        for (uint32_t w = 0; w < nw; ++w) get(&mst[gi][(size_t)w * g.kstride + idx], 8);
+      }
+    }
+  } else if (!a->mqs.empty()) {
+    return fail(a, CEP_E_STATE, "snapshot has no multi-query group state (version < 5)");
+  }
   // Phase 2: commit (device allocations first, so a failure leaves the
   // runtime as it was)
   auto& r = a->ro;
@@ -2013,6 +2545,8 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
     if (!km[pi].rev.empty()) hipMemcpy(rt.krev.p, km[pi].rev.data(), km[pi].rev.size() * 8, hipMemcpyHostToDevice);
     hipMemcpy(rt.kcount.p, km[pi].cnt, 8, hipMemcpyHostToDevice);
   }
+  for (size_t gi = 0; gi < a->mqs.size(); ++gi)
+    hipMemcpy(a->mqs[gi].state.p, mst[gi].data(), mst[gi].size() * 8, hipMemcpyHostToDevice);
   a->events_in = ev;
   return CEP_OK;
 }

@@ -1250,6 +1250,27 @@ void compile_single(CompiledApp* app, QueryAst& q) {
     h.outs = &out.select;
     bind_expr(q.having, h, app);
     if (q.having->t != T_BOOL) fail(CEP_E_PARSE, "having condition must be bool");
+    // `<output attribute> op constant` (either order): the multi-query walk
+    // compares the item's value without the interpreter
+    out.having_simple = false;
+    {
+      const ExprP& hx = q.having;
+      if (hx->k == Expr::BIN && hx->args.size() == 2) {
+        const std::string& op = hx->op;
+        const bool cmp = op == "==" || op == "!=" || op == "<" || op == "<=" || op == ">" || op == ">=";
+        ExprP item, k;
+        bool flip = false;
+        if (hx->args[1]->k == Expr::CONST) { item = hx->args[0]; k = hx->args[1]; }
+        else if (hx->args[0]->k == Expr::CONST) { item = hx->args[1]; k = hx->args[0]; flip = true; }
+        if (cmp && item && item->k == Expr::ATTR && item->out >= 0 && numeric(item->t) && numeric(k->t)) {
+          out.having_simple = true;
+          out.having_item = item->out;
+          out.having_ctype = promote(item->t, k->t);
+          out.having_cconst = host_convert(k->bits, k->t, out.having_ctype);
+          out.having_cop = cmp_op(op, flip);
+        }
+      }
+    }
     if (agg) {
       // output attributes inline as their select expressions, so the device
       // evaluates having over aggregates and event columns only
@@ -1366,10 +1387,13 @@ void compile_nfa(CompiledApp* app, QueryAst& q) {
     ns.stream = app->input_index(q.states[j].stream);
     ns.min_count = q.states[j].min_count;
     ns.max_count = q.states[j].max_count;
+    ns.terms.n = 0;   // no condition: always true
     if (q.states[j].cond) {
+      ns.terms.n = -1;
       if (self_only(q.states[j].cond, j)) {
         CodeGen cg(app, raw);
         ns.raw = cg.compile(q.states[j].cond);
+        ns.terms = lower_terms({q.states[j].cond});
       } else {
         const int jj = j;
         Loader wl{[&, jj](const Expr& e) {

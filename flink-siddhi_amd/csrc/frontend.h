@@ -54,6 +54,12 @@ struct Query {
   std::string out_stream;
   std::vector<OutItem> select;   // output attributes in definition order
   Prog having;                   // over LDOUT / LDCOL / LDAGG
+  // interpreter-free having (multi-query walk): `<select item> cop constant`;
+  // having_item -1 with having_simple = true: no having
+  bool having_simple = true;
+  int having_item = -1;
+  int having_cop = 0, having_ctype = 0;
+  uint64_t having_cconst = 0;
 
   // ---- filter / aggregation (single input stream)
   int in_stream = -1;
@@ -87,6 +93,7 @@ struct Query {
     int min_count = 1, max_count = 1;   // max -1: unbounded
     Prog raw;      // condition over the event's own columns (partition pass)
     Prog walk;     // condition reading earlier states (walk: LDCOL word, LDCAP capture)
+    TermList terms;   // interpreter-free form of raw (n = 0: no condition, -1: not expressible)
   };
   struct NCap {
     int state, index, word;           // index: k-th event of the state (0 = first), -1 = last

@@ -388,7 +388,113 @@ struct RouteKeyArgs {
   int32_t* chan;               // out: channel
 };
 
+// -------------------------------- multi-query groups (mq_kernels.hip) --
+// One app's keyed queries that share a partition / group-by key column and
+// whose per-event work is interpreter-free (sequences of the one-live-partial
+// shape, group-by aggregations), processed together: ONE partition pass over
+// the batch evaluates every query's conditions into a per-record bit mask
+// (conditions deduplicated per input stream), ONE walk per key bucket runs
+// all the queries over each key's records (lane = key, wave = query).
+// Records are 16 + 8 * nc bytes:
+//   w0 = ts - chunk ts base (32) | row in chunk (25) << 32 | stream (3) << 57
+//   w1 = condition bits of the row's stream (47) | always-true bit 47 | key in bucket (16) << 48
+//   w2.. = physical carried columns
+constexpr int kMqMaxQ = 64;            // queries per group
+constexpr int kMqMaxCond = 47;         // distinct conditions per input stream
+constexpr int kMqTrueBit = 47;         // record bit that is always set (condition-free states)
+constexpr int kMqMaxCarry = 4;         // logical carried columns per group
+constexpr int kMqMaxPhys = 4;          // physical carried words per record
+constexpr int kMqMaxCaps = 4;          // captures per sequence
+constexpr int kMqMaxSel = 8;           // select items per query
+constexpr int kMqMaxAggs = 4;
+constexpr int kMqTile = 4096;          // rows per partition tile (1024 lanes x 4)
+constexpr int kMqPartThreads = 1024;
+constexpr int kMqWalkThreads = 1024;   // 16 waves; one workgroup per CU
+constexpr int kMqWindow = 4096;        // records per walk window (LDS)
+constexpr int kMqMaxTiles = (16 << 20) / kMqTile;   // chunk <= 16 Mi rows
+constexpr int kMqMaxKpb = 1024;        // keys per bucket
+constexpr int kMqMaxBuckets = 8192;
+enum : int32_t { MQ_SEQ = 0, MQ_AGG = 1 };
+enum : int32_t { MQ_SRC_KEY = 14, MQ_SRC_TS = 15 };   // capture / carried sources beside words 0..3
+
+struct MqCond {                   // one distinct condition of one input stream
+  TermList tl;
+  int32_t slot[kMaxTerms];        // prefetched column slot of each term
+};
+
+// Per-query descriptor (device array; read with wave-uniform indices).
+struct MqQuery {
+  int32_t kind;                   // MQ_SEQ / MQ_AGG
+  int32_t nwords;                 // state words per key
+  int64_t st_off;                 // first state word (state + st_off * kstride + w * kstride + key idx)
+  // sequence: states packed per field (state j at bits j * width)
+  int32_t nstates, every;
+  int64_t within;                 // -1: none
+  uint32_t stream_mask;           // input handles the query reads
+  uint32_t st_stream;             // 3 bits per state
+  uint64_t st_bit;                // 6 bits per state: record condition bit
+  uint64_t st_min, st_max;        // 8 bits per state; max 255 = unbounded
+  uint32_t tail_opt;              // bit j: every state after j is optional
+  int32_t ncap;
+  int32_t cap_state[kMqMaxCaps], cap_last[kMqMaxCaps], cap_src[kMqMaxCaps];   // src: logical word / MQ_SRC_*
+  // aggregation
+  int32_t in_stream, filter_bit, nagg;
+  int32_t agg_fn[kMqMaxAggs], agg_arg_type[kMqMaxAggs], agg_out_type[kMqMaxAggs], agg_src[kMqMaxAggs];
+  int32_t hav_item, hav_cop, hav_ctype;   // hav_item -1: no having
+  uint64_t hav_cconst;
+  // select items: SRC_KEY, SRC_CAP + i (sequence), SRC_AGG + i, SRC_REC + logical word (aggregation)
+  int32_t nsel;
+  int32_t sel_src[kMqMaxSel], sel_type[kMqMaxSel];
+  // output stream (rewritten when the engine grows it)
+  void* out_col[kMqMaxSel];
+  int64_t* out_ts;
+  int64_t* out_seq;
+  unsigned long long* out_count;
+  int64_t out_cap;
+};
+
+struct MqPartArgs {
+  RowsArgs rows;
+  PrefPlan pref;                  // prefetched columns: key, condition columns, carried columns
+  int32_t ts_slot;                // slot whose column IS the event-ts buffer (-1: none)
+  uint32_t stream_mask;           // input handles some group query reads
+  int32_t key_slot;               // slot of the key column
+  int32_t ncond[8];               // conditions per input handle
+  const MqCond* conds;            // [8][kMqMaxCond]
+  int32_t nphys;                  // physical carried words
+  int32_t phys_slot[kMqMaxPhys];  // slot of physical carried word w
+  int32_t check_order;            // 1: some query has `within` (ts order check)
+  int64_t key_capacity;
+  int32_t key_stride, key_offset;
+  int32_t buckets_log2;
+  int32_t ntiles;
+  int64_t* chunk_base;            // out: {ts, seq} of the chunk's first row
+  uint64_t* recs;                 // out: tile t at recs + t * kMqTile * (2 + nphys)
+  uint16_t* tile_off;             // out: [P + 1][ntiles] bucket-major exclusive offsets
+  unsigned int* err;
+};
+
+struct MqWalkArgs {
+  const MqQuery* q;
+  int32_t nq;
+  int32_t nphys;
+  int32_t lmap[kMqMaxCarry];      // logical carried word -> physical word, -1: the event ts
+  const uint64_t* recs;
+  const uint16_t* tile_off;
+  int32_t ntiles;
+  int32_t buckets_log2;
+  int32_t kpb;                    // keys per bucket
+  int32_t key_stride, key_offset;
+  const int64_t* chunk_base;
+  const int64_t* in_seq;          // per-row arrival numbers of the chunk (row shuffle), or nullptr
+  uint64_t* state;                // per-query SoA state words over the bucket-major key index
+  int64_t kstride;
+  unsigned int* err;
+};
+
 // --------------------------------------------------------------- launchers --
+void launch_mq_partition(const MqPartArgs& a, hipStream_t s);
+void launch_mq_walk(const MqWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_keymap(const KeyMapArgs& a, hipStream_t s);

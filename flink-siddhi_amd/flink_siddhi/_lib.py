@@ -29,7 +29,8 @@ TYPE_NAMES = {INT: "int", LONG: "long", FLOAT: "float", DOUBLE: "double",
 NUMPY_DTYPES = {INT: "int32", LONG: "int64", FLOAT: "float32",
                 DOUBLE: "float64", BOOL: "uint8", STRING: "int32"}
 
-K_FILTER, K_PARTITION, K_WALK, K_ROUTE, K_ORDER, K_AGG, K_OTHER, K_CF_PARTITION, K_CF_WALK, K_HOT = range(10)
+(K_FILTER, K_PARTITION, K_WALK, K_ROUTE, K_ORDER, K_AGG, K_OTHER, K_CF_PARTITION, K_CF_WALK, K_HOT,
+ K_MQ_PARTITION, K_MQ_WALK) = range(12)
 
 
 # ---- exceptions mirroring the reference ---------------------------------

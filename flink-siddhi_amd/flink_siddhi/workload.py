@@ -141,6 +141,43 @@ def rows_digest(k, p1, p2, t, seq) -> int:
     return int(x.sum().item()) & ((1 << 64) - 1)
 
 
+def _key_ranks(k64):
+    """Rank of every row among the rows of its key, in row order."""
+    import torch
+    n = int(k64.shape[0])
+    order = torch.argsort(k64, stable=True)
+    ks = k64[order]
+    idx = torch.arange(n, device=k64.device, dtype=torch.int64)
+    start = torch.zeros(n, dtype=torch.bool, device=k64.device)
+    start[0] = True
+    start[1:] = ks[1:] != ks[:-1]
+    first = torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), 0).values
+    rank = torch.empty_like(idx)
+    rank[order] = idx - first
+    return rank
+
+
+def rows_digest_words(key, cols, ts, seq) -> int:
+    """Order-sensitive digest of any output stream's rows (torch tensors,
+    rows in emission order): sum over rows of oracle/mq_oracle.c
+    mq_row_digest(key, rank among the key's rows, every select column as a
+    64-bit word — ints sign-extended, doubles as their bits — , ts, seq)."""
+    import torch
+    n = int(ts.shape[0])
+    if n == 0:
+        return 0
+    k64 = key.to(torch.int64)
+    x = _smix_t((k64 & 0xFFFFFFFF) | (_key_ranks(k64) << 32))
+    for c in cols:
+        c = c.contiguous()
+        w = c.view(torch.int64) if c.dtype == torch.float64 else \
+            c.view(torch.int32).to(torch.int64) if c.dtype == torch.float32 else c.to(torch.int64)
+        x = _smix_t(x ^ w)
+    x = _smix_t(x ^ ts.to(torch.int64))
+    x = _smix_t(x ^ seq.to(torch.int64))
+    return int(x.sum().item()) & ((1 << 64) - 1)
+
+
 def generate_device(first: int, n: int, keys: int, rate: int = 400, seed: int = SEED,
                     t0: int = T0, single_stream: bool = False, device="cuda"):
     """Same stream, generated on the GPU into torch tensors (bench inputs)."""

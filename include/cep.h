@@ -152,7 +152,8 @@ enum {
   CEP_K_FILTER = 0, CEP_K_PARTITION = 1, CEP_K_WALK = 2, CEP_K_ROUTE = 3,
   CEP_K_ORDER = 4, CEP_K_AGG = 5, CEP_K_OTHER = 6,
   CEP_K_CF_PARTITION = 7, CEP_K_CF_WALK = 8,  /* closed-form fast path (k_cfpart / k_cfwalk) */
-  CEP_K_HOT = 9                               /* hot-key matching (hot.hip, one entry per chunk) */
+  CEP_K_HOT = 9,                              /* hot-key matching (hot.hip, one entry per chunk) */
+  CEP_K_MQ_PARTITION = 10, CEP_K_MQ_WALK = 11  /* multi-query groups (k_mqpart / k_mqwalk) */
 };
 
 /* ---- plan-level calls (no device needed) ------------------------------ */

@@ -167,3 +167,56 @@ def test_row_shuffle_rejects_unkeyed_state():
     with pytest.raises(fs.UnsupportedPlanException, match="not keyed"):
         rt.row_words()
     rt.shutdown()
+
+
+def _cores():
+    import os
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _digests(rt, outs, parts):
+    """Append this flush's device rows of every output (clones) to parts."""
+    for o in outs:
+        ts, seq, cols = rt.output_tensors(o, copy=True)
+        parts[o].append((ts, seq, cols))
+
+
+def _digest_of(parts):
+    import torch
+    ts = torch.cat([p[0] for p in parts])
+    seq = torch.cat([p[1] for p in parts])
+    cols = [torch.cat([p[2][c] for p in parts]) for c in range(len(parts[0][2]))]
+    return int(ts.shape[0]), workload.rows_digest_words(cols[0], cols, ts, seq)
+
+
+def test_config5_bench_geometry_vs_c_oracle():
+    """BASELINE config 5 at the bench geometry: K = 2^20 keys, R = 400
+    events/ms, 16 Mi-event chunks, 2^25 events in two batches (state carries
+    across the flush), every one of the 64 outputs compared with
+    oracle/mq_oracle.c by row count and order-sensitive digest (per-key order,
+    every select word, ts, seq)."""
+    import torch
+    import cep_oracle as CO
+    K, n = 1 << 20, 1 << 25
+    outs = workload.CONFIG5_OUTPUTS
+    rt = fs.SiddhiAppRuntime(workload.config5_plan(), key_capacity=K, chunk_events=1 << 24,
+                             pending_slots=4, ordered_output=0)
+    parts = {o: [] for o in outs}
+    h = n // 2
+    for s, e in ((0, h), (h, n)):
+        d = workload.generate_device(s, e - s, K, rate=400)
+        d["stream"] = workload.config5_streams(d["price"]).to(torch.uint8)
+        rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
+        _digests(rt, outs, parts)
+        rt.reset_output()
+        del d
+    rt.shutdown()
+    got = {o: _digest_of(parts[o]) for o in outs}
+    del parts
+    torch.cuda.empty_cache()
+    w = CO.generate(0, n, K, rate=400, threads=_cores())
+    w["stream"] = workload.config5_streams(w["price"]).astype(np.uint8)
+    cnt, dig, _ = CO.mq_mt(CO.config5_queries(), w, K, threads=_cores())
+    bad = [(o, got[o], (cnt[i], dig[i])) for i, o in enumerate(outs) if got[o] != (cnt[i], dig[i])]
+    assert not bad, bad[:4]
+    assert sum(cnt[:32]) > 5000 and sum(cnt[32:]) > 10 ** 8, (sum(cnt[:32]), sum(cnt[32:]))
