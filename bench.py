@@ -51,7 +51,8 @@ PATTERN_OUT_BYTES = PATTERN_SEL_BYTES + 8 + 8   # + event ts + arrival seq the e
 CF_REC_BYTES = 16                         # closed-form record (w0 + one carried word)
 CF_STATE_BYTES = 2 * (4 + 16)             # per key per walk launch: header + slot 0 (ts, p1), read + write
 FILTER_IN_BYTES = 4 + 8                   # id, price per event
-FILTER_OUT_BYTES = 4 + 4 + 8 + 8 + 8 + 8  # id, name, price, timestamp + event ts + seq
+FILTER_OUT_BYTES = 4 + 4 + 8 + 8 + 8 + 8  # id, name, price, timestamp + event ts + seq (design)
+FILTER_SEL_BYTES = 4 + 4 + 8 + 8          # id, name, price, timestamp (24 B per selected row)
 
 
 def parse():
@@ -77,6 +78,8 @@ def parse():
                          "ordinary host memory) instead of device-resident inputs")
     ap.add_argument("--deliver", action="store_true",
                     help="deliver every match to a host callback at each flush (pinned D2H)")
+    ap.add_argument("--parity-steps", type=int, default=4,
+                    help="config 5: steps of the stream the parity check covers (fresh state)")
     return ap.parse_args()
 
 
@@ -284,36 +287,62 @@ def cpu_baseline_filter(w):
 
 
 # ---------------------------------------------------------------- config 5 --
-def config5_parity(args, opts, n_check=20000):
-    """The bench stream's first n_check events through a fresh runtime vs the
-    Python oracle (oracle/siddhi_oracle.py: sequences and aggregates are not
-    in the C restatement), every output stream row for row."""
+C5_SEQ_SEL_BYTES = 4 + 8 + 8 + 8    # Seq<q>: k, p1, p2, t3
+C5_AGG_SEL_BYTES = 4 + 8 + 8        # Agg<q>: k, total, n
+
+
+def config5_parity(args, opts, n, steps):
+    """A fresh runtime over the bench stream's first `steps` steps (n events
+    each, output read per step as the bench flushes it) vs oracle/mq_oracle.c
+    sharded by key over the host cores on the same events: every one of the
+    64 outputs by row count and order-sensitive digest (per-key order, every
+    select word, ts, seq).  The oracle's processing time is the CPU baseline
+    (kind "port": the Java reference cannot run in this image)."""
     import numpy as np
+    import torch
     import flink_siddhi as fs
     from flink_siddhi import workload
     sys.path.insert(0, str(ROOT / "oracle"))
-    sys.path.insert(0, str(ROOT / "tests"))
-    from helpers import engine_rows, oracle_run
-    plan = workload.config5_plan()
-    w = workload.generate(0, n_check, args.keys, rate=args.rate)
+    import cep_oracle as CO
+    outs = workload.CONFIG5_OUTPUTS
+    rt = fs.SiddhiAppRuntime(workload.config5_plan(), **dict(opts, profile=0))
+    base = {o: torch.zeros(args.keys, dtype=torch.int64, device="cuda") for o in outs}
+    cnt = {o: 0 for o in outs}
+    dig = {o: 0 for o in outs}
+    for s in range(steps):
+        d = workload.generate_device(s * n, n, args.keys, rate=args.rate)
+        d["k"] = remap_keys(args, d["k"])
+        d["stream"] = workload.config5_streams(d["price"]).to(torch.uint8)
+        rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
+        for o in outs:
+            ts, seq, cols = rt.output_tensors(o, copy=False)
+            cnt[o] += int(ts.shape[0])
+            dig[o] = (dig[o] + workload.rows_digest_words(cols[0], cols, ts, seq, base[o])) & ((1 << 64) - 1)
+        rt.reset_output()
+        del d
+    rt.shutdown()
+    del base
+    torch.cuda.empty_cache()
+    T, naff, quota = host_cores()
+    w = CO.generate(0, steps * n, args.keys, rate=args.rate, threads=T)
     w["k"] = remap_keys(args, w["k"])
     w["stream"] = workload.config5_streams(w["price"]).astype(np.uint8)
-    rt = fs.SiddhiAppRuntime(plan, **dict(opts, profile=0, ordered_output=1))
-    for o in workload.CONFIG5_OUTPUTS:
-        rt.add_callback(o)
-    rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
-    rt.flush()
-    got = {o: engine_rows(rt.collect(o)) for o in workload.CONFIG5_OUTPUTS}
-    rt.shutdown()
-    names = "ABC"
-    ev = [(names[s], t, (k, t, i, p)) for k, t, i, p, s in
-          zip(w["k"].tolist(), w["ts"].tolist(), w["id"].tolist(), w["price"].tolist(), w["stream"].tolist())]
-    want = oracle_run(plan, ev)
-    bad = [o for o in workload.CONFIG5_OUTPUTS if got[o] != want.get(o, [])]
-    rows = sum(len(v) for v in got.values())
-    return {"parity": "ok" if not bad else "MISMATCH", "events": n_check, "rows": rows,
-            "mismatched_outputs": bad[:8],
-            "checker": "oracle/siddhi_oracle.py (Python restatement), every output, emission order"}
+    wc, wd, sec = CO.mq_mt(CO.config5_queries(), w, args.keys, threads=T)
+    bad = [o for i, o in enumerate(outs) if (cnt[o], dig[o]) != (wc[i], wd[i])]
+    seq_rows = sum(wc[:32])
+    agg_rows = sum(wc[32:])
+    res = {"parity": "ok" if not bad else "MISMATCH", "events": steps * n, "steps": steps,
+           "rows": sum(cnt.values()), "seq_rows": seq_rows, "agg_rows": agg_rows,
+           "mismatched_outputs": bad[:8],
+           "checker": "oracle/mq_oracle.c mq_run_mt (fresh state, events [0, %d)): every output's row count "
+                      "and order-sensitive digest" % (steps * n)}
+    cpu = {"value": round(steps * n / sec, 1), "unit": "events/s", "cores": T, "kind": "port",
+           "sample": "events [0, %d) of the config-5 stream (K=%d, R=%d/ms), oracle/mq_oracle.c sharded by key "
+                     "over %d threads (affinity %d CPUs, cgroup quota %s), %d rows, %.2f s"
+                     % (steps * n, args.keys, args.rate, T, naff, "none" if quota is None else "%.1f" % quota,
+                        seq_rows + agg_rows, sec)}
+    sel = (C5_SEQ_SEL_BYTES * seq_rows + C5_AGG_SEL_BYTES * agg_rows) / max(1, seq_rows + agg_rows)
+    return res, cpu, sel
 
 
 # ------------------------------------------------------------------- main --
@@ -348,9 +377,14 @@ def main():
 
     # parity + CPU baseline first (N=1): the host leg needs the same events
     parity, cpu, kept = None, None, None
+    c5_sel = C5_AGG_SEL_BYTES
     if config5:
-        if world == 1 and not args.no_parity:
-            parity = config5_parity(args, opts)
+        if world == 1 and not (args.no_parity and args.no_cpu):
+            parity, cpu, c5_sel = config5_parity(args, opts, n, args.parity_steps)
+            if args.no_parity:
+                parity = None
+            if args.no_cpu:
+                cpu = None
     elif world == 1 and not (args.no_parity and args.no_cpu):
         if pattern:
             parity, w, kept = pattern_parity(args, n, opts)
@@ -469,7 +503,8 @@ def main():
     # per-kernel HIP-event times on the engine's stream over the timed region
     kern = {}
     for k, name in ((L.K_PARTITION, "k_partition"), (L.K_WALK, "k_walk"), (L.K_FILTER, "k_filter"),
-                    (L.K_ROUTE, "k_route"), (L.K_CF_PARTITION, "k_cfpart"), (L.K_CF_WALK, "k_cfwalk")):
+                    (L.K_ROUTE, "k_route"), (L.K_CF_PARTITION, "k_cfpart"), (L.K_CF_WALK, "k_cfwalk"),
+                    (L.K_MQ_PARTITION, "k_mqpart"), (L.K_MQ_WALK, "k_mqwalk")):
         launches = st1.kernel_launches[k] - st0.kernel_launches[k]
         timed = st1.kernel_timed[k] - st0.kernel_timed[k]
         ms = st1.kernel_ms[k] - st0.kernel_ms[k]
@@ -479,15 +514,21 @@ def main():
     m_per_event = (st1.matches_out - st0.matches_out) / float(n * steps)
     ev_total = float(n * steps)
     keys_local = (args.keys + world - 1) // world
+    # SURVEY §8(d) algorithmic bytes per event: the columns the workload reads
+    # once + the selected attributes of every output row
     if pattern:
-        # Pipeline (headline): SURVEY §8(d)'s algorithmic bytes per event —
-        # the 25 B the pattern reads + 28 B per selected match row — over the
-        # whole step.  Per kernel: the bytes each kernel must move in this
-        # design (k_cfpart: input + records; k_cfwalk: records + output rows +
-        # per-key state), per launch.
         alg_per_event = PATTERN_IN_BYTES + PATTERN_SEL_BYTES * m_per_event
-        kept = kept if kept is not None else 0.33
-        total_bytes = {
+    elif config5:
+        alg_per_event = PATTERN_IN_BYTES + c5_sel * m_per_event
+    else:
+        alg_per_event = FILTER_IN_BYTES + FILTER_SEL_BYTES * m_per_event   # 13.92 B at 8 % selectivity
+    # Design bytes (diagnostic): what each kernel of this implementation must
+    # move per launch — its inputs, records it writes / reads, output rows
+    # with their ts / seq, per-key state.
+    kept = kept if kept is not None else 0.33
+    design = {}
+    if pattern:
+        design = {
             "k_cfpart": ev_total * (PATTERN_IN_BYTES + CF_REC_BYTES * kept),
             "k_cfwalk": ev_total * (CF_REC_BYTES * kept + PATTERN_OUT_BYTES * m_per_event),
             "k_partition": ev_total * PATTERN_IN_BYTES,
@@ -495,36 +536,42 @@ def main():
         }
         for k in ("k_cfwalk", "k_walk"):
             if k in kern:
-                total_bytes[k] += kern[k]["launches"] * keys_local * CF_STATE_BYTES
+                design[k] += kern[k]["launches"] * keys_local * CF_STATE_BYTES
         if shuffle_mode:
-            total_bytes["k_route"] = ev_total * PATTERN_IN_BYTES
+            design["k_route"] = ev_total * PATTERN_IN_BYTES
     elif config5:
-        # one pass over the 25 B/event the queries read, plus every output row
-        # (~36 B: key, two f64 / i64 values, ts, seq); per kernel: each of the
-        # 64 queries' partition passes re-reads the columns it needs
-        alg_per_event = PATTERN_IN_BYTES + 36 * m_per_event
-        total_bytes = {"k_partition": ev_total * PATTERN_IN_BYTES * 64}
+        rec = 8 * (2 + 1)   # k_mqpart record: w0, w1, price (the ts column aliases the event ts)
+        st_words = 32 * 4 + 32 * 3
+        design = {"k_mqpart": ev_total * (PATTERN_IN_BYTES + rec),
+                  "k_mqwalk": ev_total * (rec + (c5_sel + 16) * m_per_event)}
+        if "k_mqwalk" in kern:
+            design["k_mqwalk"] += kern["k_mqwalk"]["launches"] * keys_local * st_words * 8 * 2
     else:
-        alg_per_event = FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event
-        total_bytes = {"k_filter": ev_total * alg_per_event}
+        design = {"k_filter": ev_total * (FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event)}
     per_kernel = {}
-    for kname, b in total_bytes.items():
+    for kname, b in design.items():
         if kname not in kern:
             continue
         per_launch = b / kern[kname]["launches"]
         ach = per_launch / (kern[kname]["avg_us"] * 1e-6) / 1e9
-        per_kernel[kname] = {"bytes_per_launch": round(per_launch), "avg_launch_us": kern[kname]["avg_us"],
-                             "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+        per_kernel[kname] = {"design_bytes_per_launch": round(per_launch), "avg_launch_us": kern[kname]["avg_us"],
+                             "design_achieved": round(ach, 1), "design_frac": round(ach / HBM_PEAK_GBS, 4),
                              "traffic": pmc_traffic(kname) if world == 1 else None}
     roofline = None
-    if per_kernel:   # CEP_PROFILE=0 (no per-kernel timer events): no kernel roofline
-        dom = max(per_kernel, key=lambda k: kern[k]["total_ms"])
-        pk = per_kernel[dom]
-        tr = pk["traffic"]
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": pk["achieved"], "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": pk["frac"],
+    if kern:   # CEP_PROFILE=0 (no per-kernel timer events): no kernel roofline
+        # the dominant kernel (largest share of the step's kernel time),
+        # credited with the §8(d) bytes of the events one launch covers
+        dom = max(kern, key=lambda k: kern[k]["total_ms"])
+        ev_launch = ev_total / kern[dom]["launches"]
+        alg_launch = alg_per_event * ev_launch
+        ach = alg_launch / (kern[dom]["avg_us"] * 1e-6) / 1e9
+        tr = pmc_traffic(dom) if world == 1 else None
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": tr["bytes_per_launch"] if tr else None,
-                    "bytes_per_launch": pk["bytes_per_launch"], "avg_launch_us": pk["avg_launch_us"]}
+                    "alg_bytes_per_event": round(alg_per_event, 3), "events_per_launch": round(ev_launch),
+                    "alg_bytes_per_launch": round(alg_launch), "avg_launch_us": kern[dom]["avg_us"],
+                    "formula": "alg_bytes_per_event * events_per_launch / avg_launch_us"}
     per_gpu_events = value / world
     pipeline = {"alg_bytes_per_event": round(alg_per_event, 3),
                 "achieved": round(per_gpu_events * alg_per_event / 1e9, 1), "unit": "GB/s",
@@ -546,7 +593,9 @@ def main():
                         "ingest": (("%s all-to-all key shuffle" % ("rccl" if _coll_device() == "cuda"
                                                                     else "gloo host-staged"))
                                     if shuffle_mode else
-                                   "pre-partitioned (keyed upstream)") if world > 1 else "local"}
+                                   "pre-partitioned (keyed upstream)") if world > 1 else
+                                  ("host (%s memory over PCIe)" % ("pinned" if args.ingest == "host" else "pageable")
+                                   if host_ingest else "device-resident")}
                        if pattern else
                        {"workload": "config5: 64 queries (32 every A, B+, C within 10 sec sequences with "
                                     "id == q%50, 32 group-by/having aggregations), 3 keyed streams",

@@ -203,6 +203,8 @@ struct MqLds {
   uint32_t seg[kMqMaxTiles + 1];         // exclusive prefix of the bucket's tile segments
   uint16_t lo[kMqMaxTiles];              // segment start inside each tile
   uint32_t scratch[kMqWalkThreads / 64 + 1];
+  int32_t wt1;                           // window end tile (-1: a split tile)
+  uint32_t nwin;                         // records of a split tile's row range
 };
 
 // Per-window view one lane needs to read its records.
@@ -526,21 +528,29 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
     if (tid == 0) L.seg[ntiles] = total;
   }
   lds_barrier();
-  const uint32_t total = L.seg[ntiles];
-  for (uint32_t wb = 0; wb < total; wb += W) {
-    const uint32_t nw = total - wb < (uint32_t)W ? total - wb : (uint32_t)W;
-    for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
-    lds_barrier();
-    // gather: window slot p = bucket record wb + p, in tile t = last with seg[t] <= wb + p
-    for (uint32_t p = tid; p < nw; p += NT) {
-      const uint32_t g = wb + p;
-      int lo = 0, hi = ntiles - 1;
+  // Windows are whole tiles [t0, t1) of at most W records; a tile whose
+  // segment alone exceeds W is split into row ranges of W rows (a tile's
+  // records are not in arrival order inside its segment, so a window never
+  // ends inside a segment by position).
+  int t0 = 0;
+  uint32_t sub = 0;   // row range of a split tile
+  while (t0 < ntiles) {
+    if (tid == 0) {
+      int lo = t0 + 1, hi = ntiles;
+      const uint32_t lim = L.seg[t0] + (uint32_t)W;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (L.seg[mid] <= g) lo = mid;
+        if (L.seg[mid] <= lim) lo = mid;
         else hi = mid - 1;
       }
-      const int64_t ri = (int64_t)lo * kMqTile + L.lo[lo] + (g - L.seg[lo]);
+      L.wt1 = L.seg[t0 + 1] - L.seg[t0] > (uint32_t)W ? -1 : lo;   // -1: split tile t0
+      L.nwin = 0;
+    }
+    for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
+    lds_barrier();
+    const int t1 = L.wt1;
+    const bool split = t1 < 0;
+    auto load = [&](uint32_t p, int64_t ri) {
       const uint64_t* rec = a.recs + ri * RW;
       const uint64_t w0 = rec[0], w1 = rec[1];
       L.w0[p] = w0;
@@ -548,8 +558,44 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
 #pragma unroll
       for (int w = 0; w < NC; ++w) L.car[p * NC + w] = rec[2 + w];
       atomicAdd(&L.kstart[mq_key(w1) + 1], 1u);
+    };
+    uint32_t nw;
+    if (!split) {
+      // gather: window slot p = bucket record seg[t0] + p, in tile t = last with seg[t] <= that
+      const uint32_t wb = L.seg[t0];
+      nw = L.seg[t1] - wb;
+      for (uint32_t p = tid; p < nw; p += NT) {
+        const uint32_t g = wb + p;
+        int lo = t0, hi = t1 - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (L.seg[mid] <= g) lo = mid;
+          else hi = mid - 1;
+        }
+        load(p, (int64_t)lo * kMqTile + L.lo[lo] + (g - L.seg[lo]));
+      }
+      lds_barrier();
+    } else {
+      // rows [t0 * T + sub * W, + W) of tile t0: at most W records
+      const uint32_t cnt = L.seg[t0 + 1] - L.seg[t0];
+      const uint32_t rlo = (uint32_t)t0 * kMqTile + sub * (uint32_t)W, rhi = rlo + (uint32_t)W;
+      for (uint32_t p = tid; p < cnt; p += NT) {
+        const int64_t ri = (int64_t)t0 * kMqTile + L.lo[t0] + p;
+        const uint32_t row = mq_row(a.recs[ri * RW]);
+        if (row >= rlo && row < rhi) load(atomicAdd(&L.nwin, 1u), ri);
+      }
+      lds_barrier();
+      nw = L.nwin;
     }
-    lds_barrier();
+    if (split) {
+      ++sub;
+      if (sub * (uint32_t)W >= (uint32_t)kMqTile) {
+        sub = 0;
+        ++t0;
+      }
+    } else {
+      t0 = t1;
+    }
     {
       const uint32_t c = tid < kpb ? L.kstart[tid + 1] : 0u;
       uint32_t tot;
@@ -644,7 +690,7 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       else mq_agg<true, NC>(c, Q, S, ks, maxlen, pos);
     }
     // the next window re-reads state this one wrote and reuses the LDS arrays
-    if (wb + W < total) __syncthreads();
+    if (t0 < ntiles) __syncthreads();
   }
 }
 

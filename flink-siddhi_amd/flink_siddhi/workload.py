@@ -157,17 +157,24 @@ def _key_ranks(k64):
     return rank
 
 
-def rows_digest_words(key, cols, ts, seq) -> int:
+def rows_digest_words(key, cols, ts, seq, rank_base=None) -> int:
     """Order-sensitive digest of any output stream's rows (torch tensors,
     rows in emission order): sum over rows of oracle/mq_oracle.c
     mq_row_digest(key, rank among the key's rows, every select column as a
-    64-bit word — ints sign-extended, doubles as their bits — , ts, seq)."""
+    64-bit word — ints sign-extended, doubles as their bits — , ts, seq).
+    rank_base (int64 tensor indexed by key, optional): rows each key had in
+    earlier parts of the same output; it is advanced by this part's rows, so
+    a stream flushed in parts digests like the whole."""
     import torch
     n = int(ts.shape[0])
     if n == 0:
         return 0
     k64 = key.to(torch.int64)
-    x = _smix_t((k64 & 0xFFFFFFFF) | (_key_ranks(k64) << 32))
+    rank = _key_ranks(k64)
+    if rank_base is not None:
+        rank = rank + rank_base[k64]
+        rank_base.index_add_(0, k64, torch.ones_like(k64))
+    x = _smix_t((k64 & 0xFFFFFFFF) | (rank << 32))
     for c in cols:
         c = c.contiguous()
         w = c.view(torch.int64) if c.dtype == torch.float64 else \

@@ -211,8 +211,9 @@ def test_restore_rejects_truncated_snapshot_and_keeps_state():
     import struct
     body = bytearray(snap)
     # reorder rows (columns k ts id price + event ts + stream), then the
-    # 1-byte key-map section of the one pattern
-    tail = len(body) - 1 - held * (4 + 8 + 4 + 8 + 8 + 1)
+    # 1-byte key-map section of the one pattern and the (v5) u32 count of
+    # multi-query groups
+    tail = len(body) - 1 - 4 - held * (4 + 8 + 4 + 8 + 8 + 1)
     n_off = tail - 8 - 8                                   # i64 n, i64 released_max precede the rows
     assert struct.unpack_from("<q", body, n_off)[0] == held
     struct.pack_into("<q", body, n_off, (1 << 31) - 1)
@@ -236,7 +237,7 @@ def test_restore_version2_snapshot():
     first = engine_rows(rt.collect("O"))
     snap = bytearray(rt.snapshot())
     rt.shutdown()
-    assert struct.unpack_from("<I", snap, 4)[0] == 4
+    assert struct.unpack_from("<I", snap, 4)[0] == 5
     # version 2 layout: no per-key pending count, no reorder section (an
     # empty one is i32 input, u8 has_stream, i64 n, i64 released_max)
     v2 = bytearray(snap[:28])
@@ -252,7 +253,7 @@ def test_restore_version2_snapshot():
             v2 += snap[off:off + 12]
             v2 += snap[off + 16:off + 16 + n * sw * 8]
             off += 16 + n * sw * 8
-    assert len(snap) - off == 22   # empty reorder section + the key-map byte
+    assert len(snap) - off == 26   # empty reorder section + the key-map byte + no groups
     rt2 = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
     rt2.add_callback("O")
     rt2.restore(bytes(v2))
