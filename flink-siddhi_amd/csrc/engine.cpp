@@ -205,6 +205,7 @@ struct cep_app {
   std::vector<char> in_mq;        // per query: served by a multi-query group
   DevBuf tile_state, ticket, err;
   DevBuf route_arena, route_tcount, route_toffs, route_dcount;   // key shuffle (sender)
+  DevBuf rerr;                 // error word of the route kernels (route stream; the walk's is `err`)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   DevBuf str_hash;             // Java String.hashCode per dictionary id (dynamic routing)
   HostBuf flush_words;         // cep_flush: error word + output cursors (pinned)
@@ -613,6 +614,15 @@ int build_mq_groups(cep_app* a) {
         for (int i = 0; i < d.nsel; ++i) d.sel_src[i] = q.select[i].src;
         d.nwords = 2 + d.ncap;
       }
+      for (int i = 0; i < d.nsel; ++i) {
+        const int src = d.sel_src[i];
+        d.sel_vi[i] = (src >= SRC_CAP && src < SRC_CAP + kMqMaxCaps) ? 1 + (src - SRC_CAP)
+                      : (src >= SRC_AGG && src < SRC_AGG + kMqMaxAggs) ? 1 + (src - SRC_AGG)
+                      : (src >= SRC_REC && src < SRC_REC + kMqMaxCarry) ? 5 + (src - SRC_REC)
+                                                                         : 0;
+        d.sel_w[i] = type_width(d.sel_type[i]);
+      }
+      d.hav_vi = d.hav_item >= 0 ? d.sel_vi[d.hav_item] : 0;
       g.stream_mask |= d.stream_mask;
       g.check_order = g.check_order || (d.kind == MQ_SEQ && d.within >= 0);
       off += d.nwords;
@@ -664,13 +674,15 @@ int create_runtime(cep_app* a) {
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
   if (!dev_ensure(&a->code, cb, a->stream, false) || !dev_ensure(&a->konst, kb, a->stream, false) ||
-      !dev_ensure(&a->err, 64, a->stream, false) || !dev_ensure(&a->ticket, 64, a->stream, false))
+      !dev_ensure(&a->err, 64, a->stream, false) || !dev_ensure(&a->rerr, 64, a->stream, false) ||
+      !dev_ensure(&a->ticket, 64, a->stream, false))
     return fail(a, CEP_E_DEVICE, "out of device memory (plan)");
   if (!app.code.empty())
     hipMemcpy(a->code.p, app.code.data(), app.code.size() * sizeof(Ins), hipMemcpyHostToDevice);
   if (!app.konst.empty())
     hipMemcpy(a->konst.p, app.konst.data(), app.konst.size() * 8, hipMemcpyHostToDevice);
   hipMemset(a->err.p, 0, 64);
+  hipMemset(a->rerr.p, 0, 64);
   for (auto& sd : app.outputs) {
     OutStream o;
     o.id = sd.id;
@@ -1092,6 +1104,10 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     pa.hot_id = divert ? (const uint16_t*)rt.hot_id.p : nullptr;
     pa.nhot = divert ? kCfHotMax : 0;
     if (overlap && rt.used[b]) hipStreamWaitEvent(side, rt.walk_done[b], 0);   // arena b is free
+    // hot keys: k_cfpart reads hot_id, which the previous chunk's
+    // k_hot_update rewrites on the main stream (walk_done is recorded after
+    // it), so with diversion candidates the partition waits for that chunk
+    if (overlap && hot && rt.used[b ^ 1]) hipStreamWaitEvent(side, rt.walk_done[b ^ 1], 0);
     {
       LaunchTimer t(a, CEP_K_CF_PARTITION, side);
       launch_cf_partition(pa, ntiles, side);
@@ -1472,10 +1488,18 @@ int check_device_error(cep_app* a) {
   return device_error(a, e);
 }
 
+int error_status(cep_app* a, unsigned int e);
+
 // Error flags read back -> status (the flags are cleared).
 int device_error(cep_app* a, unsigned int e) {
   if (!e) return CEP_OK;
   hipMemset(a->err.p, 0, 64);
+  return error_status(a, e);
+}
+
+// Status of device error flags (the flags are not touched).
+int error_status(cep_app* a, unsigned int e) {
+  if (!e) return CEP_OK;
   if (e & ERR_ORDER)   // root cause first: out-of-order input also defeats `within` pruning
     return fail(a, CEP_E_ARG, "events not in event-time order: `within` requires non-decreasing timestamps");
   if (e & ERR_PENDING)
@@ -1721,6 +1745,7 @@ void cep_destroy(cep_app* a) {
   dev_free(&a->route_dcount);
   dev_free(&a->ticket);
   dev_free(&a->err);
+  dev_free(&a->rerr);
   dev_free(&a->str_hash);
   host_free(&a->flush_words);
   for (auto& d : a->rr_col) dev_free(&d);
@@ -2009,6 +2034,9 @@ int cep_watermark(cep_app* a, int64_t mark) {
   if (rc == CEP_OK) r.released_max = std::max(r.released_max, rmax);
   // the sorted batch buffers are reused by the next watermark: finish first
   hipStreamSynchronize(a->stream);
+  if (rc == CEP_OK && late > 0 && a->opt.late_policy == 1)
+    return fail(a, CEP_E_ARG, std::to_string(late) + " late event(s) dropped (older than rows an earlier watermark "
+                              "released; the reference would hand them to Siddhi out of order)");
   return rc;
 }
 
@@ -2604,7 +2632,7 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   ra.seq0 = seq0;
   ra.arena = (uint64_t*)a->route_arena.p;
   ra.tcount = (uint32_t*)a->route_tcount.p;
-  ra.err = (unsigned int*)a->err.p;
+  ra.err = (unsigned int*)a->rerr.p;
   {
     LaunchTimer t(a, CEP_K_ROUTE, rs);
     if (fast) {
@@ -2627,7 +2655,9 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   // the per-owner counts: W words, read back on the route stream only (the
   // all-to-all's split sizes are host values); the engine stream keeps going
   std::vector<unsigned long long> dc(world);
+  unsigned int re = 0;
   hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, rs);
+  hipMemcpyAsync(&re, a->rerr.p, 4, hipMemcpyDeviceToHost, rs);
   if (hipStreamSynchronize(rs) != hipSuccess) return fail(a, CEP_E_DEVICE, "route failed");
   int64_t total = 0;
   for (int d = 0; d < world; ++d) {
@@ -2635,8 +2665,13 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
     total += (int64_t)dc[d];
   }
   if (total > b->n) return fail(a, CEP_E_DEVICE, "route produced more records than rows");
-  rc = check_device_error(a);
-  if (rc) return rc;
+  // the route kernels' own error word, read and cleared on the route stream
+  // (the walk's word belongs to cep_flush)
+  if (re) {
+    hipMemsetAsync(a->rerr.p, 0, 64, rs);
+    hipStreamSynchronize(rs);
+    return error_status(a, re);
+  }
   a->batches++;
   return CEP_OK;
 }
@@ -2768,7 +2803,7 @@ int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void
   for (int i = 0; i < 8; ++i) ra.key_col_s[i] = kc[i];
   ra.arena = (uint64_t*)a->route_arena.p;
   ra.tcount = (uint32_t*)a->route_tcount.p;
-  ra.err = (unsigned int*)a->err.p;
+  ra.err = (unsigned int*)a->rerr.p;
   {
     LaunchTimer t(a, CEP_K_ROUTE, rs);
     launch_route_rows(ra, ntiles, (uint32_t*)a->route_toffs.p, (unsigned long long*)a->route_dcount.p,
@@ -2776,7 +2811,9 @@ int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void
   }
   if (slot >= 0) hipEventRecord(a->hs[slot].free, rs);
   std::vector<unsigned long long> dc(world);
+  unsigned int re = 0;
   hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, rs);
+  hipMemcpyAsync(&re, a->rerr.p, 4, hipMemcpyDeviceToHost, rs);
   if (hipStreamSynchronize(rs) != hipSuccess) return fail(a, CEP_E_DEVICE, "row route failed");
   int64_t total = 0;
   for (int d = 0; d < world; ++d) {
@@ -2784,8 +2821,11 @@ int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void
     total += (int64_t)dc[d];
   }
   if (total > b->n) return fail(a, CEP_E_DEVICE, "route produced more rows than the batch");
-  rc = check_device_error(a);
-  if (rc) return rc;
+  if (re) {   // the route kernels' own error word (route stream)
+    hipMemsetAsync(a->rerr.p, 0, 64, rs);
+    hipStreamSynchronize(rs);
+    return error_status(a, re);
+  }
   a->batches++;
   return CEP_OK;
 }

@@ -407,7 +407,7 @@ constexpr int kMqMaxPhys = 4;          // physical carried words per record
 constexpr int kMqMaxCaps = 4;          // captures per sequence
 constexpr int kMqMaxSel = 8;           // select items per query
 constexpr int kMqMaxAggs = 4;
-constexpr int kMqTile = 4096;          // rows per partition tile (1024 lanes x 4)
+constexpr int kMqTile = 16384;         // rows per partition tile (1024 lanes x 16)
 constexpr int kMqPartThreads = 1024;
 constexpr int kMqWalkThreads = 1024;   // 16 waves; one workgroup per CU
 constexpr int kMqWindow = 4096;        // records per walk window (LDS)
@@ -442,9 +442,12 @@ struct MqQuery {
   int32_t agg_fn[kMqMaxAggs], agg_arg_type[kMqMaxAggs], agg_out_type[kMqMaxAggs], agg_src[kMqMaxAggs];
   int32_t hav_item, hav_cop, hav_ctype;   // hav_item -1: no having
   uint64_t hav_cconst;
-  // select items: SRC_KEY, SRC_CAP + i (sequence), SRC_AGG + i, SRC_REC + logical word (aggregation)
+  // select items: SRC_KEY, SRC_CAP + i (sequence), SRC_AGG + i, SRC_REC + logical word (aggregation);
+  // sel_vi: the item's slot in the walk's row value array (0 key, 1 + i capture / aggregate i,
+  // 5 + w logical carried word w), sel_w: its column width in bytes
   int32_t nsel;
-  int32_t sel_src[kMqMaxSel], sel_type[kMqMaxSel];
+  int32_t sel_src[kMqMaxSel], sel_type[kMqMaxSel], sel_vi[kMqMaxSel], sel_w[kMqMaxSel];
+  int32_t hav_vi;                 // having item's value slot
   // output stream (rewritten when the engine grows it)
   void* out_col[kMqMaxSel];
   int64_t* out_ts;

@@ -8,7 +8,7 @@
 // as restated by oracle/siddhi_oracle.py (_sequence_event, _SingleInstance)
 // and oracle/mq_oracle.c.
 //
-//   k_mqpart  one 1024-lane workgroup per 4096-row tile: key, ts, stream and
+//   k_mqpart  one 1024-lane workgroup per 16384-row tile: key, ts, stream and
 //             every column a condition or capture reads loaded once per row;
 //             every distinct condition of the row's stream (deduplicated over
 //             the group's queries) evaluated once into a bit mask; LDS
@@ -45,10 +45,16 @@ __device__ __forceinline__ uint32_t mq_key(uint64_t w1) { return (uint32_t)(w1 >
 }  // namespace
 
 // ============================================================== k_mqpart ==
+// Two passes over the tile's rows inside one workgroup, so a tile can be
+// large (16 rows per lane) without holding every column of 16 rows in
+// registers: pass A reads the key and stream of all rows (bucket + LDS rank),
+// then, after the bucket scan, pass B reads the condition / carried columns
+// four rows per lane at a time and writes the records.  Large tiles keep the
+// bucket-major tile offset table small (P / 16384 entries per row).
 template <int NP>   // prefetched columns
 __global__ __launch_bounds__(kMqPartThreads, 1) void k_mqpart(MqPartArgs a) {
-  constexpr int E = kMqTile / kMqPartThreads, NT = kMqPartThreads;
-  static_assert(NT * E == kMqTile, "tile geometry");
+  constexpr int NT = kMqPartThreads, RPL = kMqTile / kMqPartThreads, EB = 4;
+  static_assert(RPL % EB == 0 && RPL <= 32, "tile geometry");
   __shared__ uint32_t scratch[NT / 64 + 1];
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // P + 1 (dynamic)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -62,71 +68,41 @@ __global__ __launch_bounds__(kMqPartThreads, 1) void k_mqpart(MqPartArgs a) {
     a.chunk_base[0] = ts_base;
     a.chunk_base[1] = row_seq(a.rows, a.rows.row0);
   }
-  // lane-interleaved rows: lane l of wave w owns chunk rows w*64*E + 64*e + l
-  const int64_t r0 = tile * kMqTile + (int64_t)wave * 64 * E + lane;
+  // lane-interleaved rows: lane l of wave w owns chunk rows w*64*RPL + 64*e + l
+  const int64_t r0 = tile * kMqTile + (int64_t)wave * 64 * RPL + lane;
   const int64_t row0 = a.rows.row0 + r0;
   uint32_t valid = 0;
 #pragma unroll
-  for (int e = 0; e < E; ++e) valid |= (r0 + 64 * e < a.rows.n ? 1u : 0u) << e;
-  uint64_t tsv[E], pv[NP][E], mask[E];
-  uint32_t sb[E];
-  uint32_t keep = 0;
+  for (int e = 0; e < RPL; ++e) valid |= (r0 + 64 * e < a.rows.n ? 1u : 0u) << e;
+  // pass A: key and stream of every row
+  const int kc = a.pref.col[0];
+  const bool klong = a.rows.cols.t[kc] == T_LONG;
+  uint64_t kv[RPL];
+  uint32_t sv[RPL];
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    tsv[e] = 0;
-    sb[e] = 0;
-    mask[e] = 1ull << kMqTrueBit;
-  }
-  if (valid) {
-    cf_load_cols<E, NP>(a.rows, a.pref, a.ts_slot, row0, valid, tsv, sb, pv);
-    if (a.check_order) {
-      // event-time order (`within` relies on it): row r - 1 is held by the
-      // previous lane (same e), lane 63 (e - 1), or loaded
-      const int64_t before = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
-      bool bad = false;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const uint64_t up = __shfl_up(tsv[e], 1, 64);
-        const uint64_t last = e > 0 ? __shfl(tsv[e > 0 ? e - 1 : 0], 63, 64) : 0ull;
-        const int64_t prev = lane > 0 ? (int64_t)up : (e > 0 ? (int64_t)last : before);
-        if ((valid >> e) & 1u) bad |= (int64_t)tsv[e] < prev;
-      }
-      if (bad) set_err(a.err, ERR_ORDER);
-    }
-    // every distinct condition of each stream, once per row (uniform loops)
-    for (int s = 0; s < 8; ++s) {
-      if (!((a.stream_mask >> s) & 1u)) continue;
-      uint32_t is_s = 0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) is_s |= (((valid >> e) & 1u) && sb[e] == (uint32_t)s ? 1u : 0u) << e;
-      keep |= is_s;
-      const int nc = a.ncond[s];
-      if (!__ballot(is_s != 0) || nc == 0) continue;
-      const MqCond* cs = a.conds + s * kMqMaxCond;
-      for (int c = 0; c < nc; ++c) {
-        const uint32_t bits = eval_terms_regs<E, NP>(cs[c].tl, cs[c].slot, a.rows.cols, pv) & is_s;
-#pragma unroll
-        for (int e = 0; e < E; ++e) mask[e] |= (uint64_t)((bits >> e) & 1u) << c;
-      }
-    }
+  for (int e = 0; e < RPL; ++e) {
+    const bool ok = (valid >> e) & 1u;
+    const int64_t rr = row0 + 64 * e;
+    kv[e] = !ok ? 0ull : klong ? ((const uint64_t*)a.rows.cols.p[kc])[rr]
+                               : from_i32(((const int32_t*)a.rows.cols.p[kc])[rr]);
+    sv[e] = (ok && a.rows.stream) ? (uint32_t)a.rows.stream[rr] : (uint32_t)a.rows.input;
   }
   lds_barrier();   // hist zeroed
-  // bits 0-12 rank in tile, 13-25 bucket
-  uint32_t packed[E], lkey[E];
+  // bits 0-14 rank in tile, 15-27 bucket; lkey: key within its bucket
+  uint32_t packed[RPL], lkey[RPL];
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < RPL; ++e) {
     packed[e] = 0xffffffffu;
     lkey[e] = 0;
-    if (!((keep >> e) & 1u)) continue;
-    const int64_t kfield = shard_key((int64_t)pv[0][e], a.key_stride, a.key_offset);   // key: slot 0
+    if (!((valid >> e) & 1u) || !((a.stream_mask >> sv[e]) & 1u)) continue;
+    const int64_t kfield = shard_key((int64_t)kv[e], a.key_stride, a.key_offset);
     if (kfield < 0 || kfield >= a.key_capacity) {
       set_err(a.err, ERR_KEY_RANGE);
       continue;
     }
     const uint32_t bucket = (uint32_t)(kfield & (P - 1));
     lkey[e] = (uint32_t)(kfield >> lg);
-    const uint32_t rank = atomicAdd(&hist[bucket], 1u);
-    packed[e] = (bucket << 13) | rank;
+    packed[e] = (bucket << 15) | atomicAdd(&hist[bucket], 1u);
   }
   lds_barrier();
   {
@@ -153,22 +129,69 @@ __global__ __launch_bounds__(kMqPartThreads, 1) void k_mqpart(MqPartArgs a) {
     if (tid == 0) hist[P] = total;
   }
   lds_barrier();
-  uint64_t* trecs = a.recs + tile * (int64_t)kMqTile * RW;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    if (packed[e] == 0xffffffffu) continue;
-    const uint32_t b = packed[e] >> 13;
-    const uint32_t slot = hist[b] + (packed[e] & 0x1fffu);
-    const int64_t dts = (int64_t)tsv[e] - ts_base;
-    if (dts < 0 || dts > 0xffffffffll) set_err(a.err, ERR_ORDER);
-    uint64_t* g = trecs + (int64_t)slot * RW;
-    g[0] = (uint64_t)(uint32_t)dts | ((uint64_t)(uint32_t)(r0 + 64 * e) << 32) | ((uint64_t)sb[e] << 57);
-    g[1] = mask[e] | ((uint64_t)lkey[e] << 48);
-#pragma unroll
-    for (int w = 0; w < kMqMaxPhys; ++w)
-      if (w < a.nphys) g[2 + w] = pick<E, NP>(pv, a.phys_slot[w], e);
-  }
   for (int i = tid; i <= P; i += NT) a.tile_off[(int64_t)i * a.ntiles + tile] = (uint16_t)hist[i];
+  // pass B: conditions and carried columns, EB rows per lane at a time
+  uint64_t* trecs = a.recs + tile * (int64_t)kMqTile * RW;
+  // predecessor of the lane's first row (read by lanes that hold rows only:
+  // row0 - 1 of a lane past the batch end would read past the ts column)
+  int64_t prev_last = 0;
+  if (valid & 1u) prev_last = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
+#pragma unroll
+  for (int g = 0; g < RPL / EB; ++g) {
+    const uint32_t vg = (valid >> (EB * g)) & ((1u << EB) - 1u);
+    uint64_t tsv[EB], pv[NP][EB], mask[EB];
+    uint32_t sb[EB];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) mask[e] = 1ull << kMqTrueBit;
+    if (__ballot(vg != 0)) {
+      cf_load_cols<EB, NP>(a.rows, a.pref, a.ts_slot, row0 + 64 * EB * g, vg, tsv, sb, pv);
+      if (a.check_order) {
+        // event-time order (`within` relies on it): row r - 1 is held by the
+        // previous lane (same e) or lane 63 (e - 1, possibly of the last round)
+        bool bad = false;
+#pragma unroll
+        for (int e = 0; e < EB; ++e) {
+          const uint64_t up = __shfl_up(tsv[e], 1, 64);
+          const uint64_t last = e > 0 ? __shfl(tsv[e > 0 ? e - 1 : 0], 63, 64) : 0ull;
+          const int64_t pl = e > 0 ? (int64_t)last : prev_last;
+          const int64_t prev = lane > 0 ? (int64_t)up : pl;
+          if ((vg >> e) & 1u) bad |= (int64_t)tsv[e] < prev;
+        }
+        if (bad) set_err(a.err, ERR_ORDER);
+        prev_last = (int64_t)__shfl(tsv[EB - 1], 63, 64);
+      }
+      // every distinct condition of each stream, once per row (uniform loops)
+      for (int s = 0; s < 8; ++s) {
+        if (!((a.stream_mask >> s) & 1u)) continue;
+        uint32_t is_s = 0;
+#pragma unroll
+        for (int e = 0; e < EB; ++e) is_s |= (((vg >> e) & 1u) && sb[e] == (uint32_t)s ? 1u : 0u) << e;
+        const int nc = a.ncond[s];
+        if (!__ballot(is_s != 0) || nc == 0) continue;
+        const MqCond* cs = a.conds + s * kMqMaxCond;
+        for (int c = 0; c < nc; ++c) {
+          const uint32_t bits = eval_terms_regs<EB, NP>(cs[c].tl, cs[c].slot, a.rows.cols, pv) & is_s;
+#pragma unroll
+          for (int e = 0; e < EB; ++e) mask[e] |= (uint64_t)((bits >> e) & 1u) << c;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EB; ++e) {
+        const int ee = EB * g + e;
+        if (packed[ee] == 0xffffffffu) continue;
+        const uint32_t b = packed[ee] >> 15;
+        const uint32_t slot = hist[b] + (packed[ee] & 0x7fffu);
+        const int64_t dts = (int64_t)tsv[e] - ts_base;
+        if (dts < 0 || dts > 0xffffffffll) set_err(a.err, ERR_ORDER);
+        uint64_t* gp = trecs + (int64_t)slot * RW;
+        gp[0] = (uint64_t)(uint32_t)dts | ((uint64_t)(uint32_t)(r0 + 64 * ee) << 32) | ((uint64_t)sb[e] << 57);
+        gp[1] = mask[e] | ((uint64_t)lkey[ee] << 48);
+#pragma unroll
+        for (int w = 0; w < kMqMaxPhys; ++w)
+          if (w < a.nphys) gp[2 + w] = pick<EB, NP>(pv, a.phys_slot[w], e);
+      }
+    }
+  }
 }
 
 void launch_mq_partition(const MqPartArgs& a, hipStream_t s) {
@@ -198,6 +221,8 @@ struct MqLds {
   uint32_t kstart[kMqMaxKpb + 1];
   uint32_t kcur[kMqMaxKpb];
   uint32_t bmax[kMqMaxKpb / 64];         // longest key run per 64-key block
+  uint16_t korder[kMqMaxKpb];            // keys by descending run length (lane blocks of alike runs)
+  uint32_t lhist[257];                   // run-length bins (descending), then their cursors
   uint32_t qoff[kMqMaxQ * (kMqMaxKpb / 64)];   // per (query, block): rows, then first row
   unsigned long long qbase[kMqMaxQ];
   uint32_t seg[kMqMaxTiles + 1];         // exclusive prefix of the bucket's tile segments
@@ -207,24 +232,31 @@ struct MqLds {
   uint32_t nwin;                         // records of a split tile's row range
 };
 
+// Descriptors are read through the constant address space: wave-uniform
+// scalar loads the compiler may keep in SGPRs across the loops (a generic
+// pointer would be reloaded after every output store it might alias).
+typedef __attribute__((address_space(4))) const MqQuery CMqQuery;
+
 // Per-window view one lane needs to read its records.
 template <int NC>
 struct MqCtx {
-  const MqLds<NC>* L;
-  const MqWalkArgs* a;
   int64_t ts_base, seq_base;
   int64_t keyv;       // the lane's partition key value
   uint32_t r0, len;   // the lane's key run in `sorted`
+  int32_t lmap0, lmap1, lmap2, lmap3;   // logical carried word -> physical (-1: event ts)
+  const int64_t* in_seq;
+  unsigned int* err;
 };
 
-// Logical carried word `src` of window record r (MQ_SRC_*: key / event ts).
+// Logical carried word `src` (uniform) of window record r (MQ_SRC_*: key /
+// event ts).
 template <int NC>
-__device__ __forceinline__ uint64_t mq_src(const MqCtx<NC>& c, int src, int r, int64_t ts) {
+__device__ __forceinline__ uint64_t mq_src(const MqLds<NC>& L, const MqCtx<NC>& c, int src, int r, int64_t ts) {
   if (src == MQ_SRC_KEY) return (uint64_t)c.keyv;
   if (src == MQ_SRC_TS) return (uint64_t)ts;
-  const int w = c.a->lmap[src];
+  const int w = src == 0 ? c.lmap0 : src == 1 ? c.lmap1 : src == 2 ? c.lmap2 : c.lmap3;
   if (w < 0) return (uint64_t)ts;   // the column is the event-ts buffer
-  if constexpr (NC > 0) return c.L->car[r * NC + (NC > 1 ? w : 0)];   // w < NC (host-checked)
+  if constexpr (NC > 0) return L.car[r * NC + (NC > 1 ? w : 0)];   // w < NC (host-checked)
   return 0;
 }
 
@@ -233,15 +265,44 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-// One sequence query over the 64 keys of a block (lane = key): restates
+// Output row p of a query from its value slots (MqQuery::sel_vi: 0 the key,
+// 1 + i capture / aggregate i, 5 + w carried word w): one uniform-indexed
+// register read and one store per column, unrolled.
+__device__ __forceinline__ void mq_store_row(CMqQuery& Q, int nsel, unsigned long long p, const uint64_t (&vals)[9],
+                                             int64_t ts, int64_t seq) {
+#pragma unroll
+  for (int x = 0; x < kMqMaxSel; ++x) {
+    if (x >= nsel) break;
+    const uint64_t v = vals[Q.sel_vi[x]];
+    const int w = Q.sel_w[x];
+    if (w == 8) ((uint64_t*)Q.out_col[x])[p] = v;
+    else if (w == 4) ((uint32_t*)Q.out_col[x])[p] = (uint32_t)v;
+    else ((uint8_t*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
+  }
+  Q.out_ts[p] = ts;
+  Q.out_seq[p] = seq;
+}
+
+// One sequence query over a block of 64 keys (lane = key): restates
 // oracle/mq_oracle.c sequence_event for the one-partial shape.  kEmit =
 // false: returns the rows the wave would emit; true: stores them from `pos`
 // and commits the state.
 template <bool kEmit, int NC>
-__device__ uint32_t mq_seq(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, int64_t ks, uint32_t maxlen,
-                           unsigned long long pos) {
-  const MqLds<NC>& L = *c.L;
-  const int N = Q.nstates;
+__device__ __forceinline__ uint32_t mq_seq(const MqLds<NC>& L, const MqCtx<NC>& c, CMqQuery& Q, uint64_t* S,
+                                           int64_t ks, uint32_t maxlen, unsigned long long pos) {
+  // the descriptor, decoded once (uniform: scalar registers)
+  const int N = Q.nstates, ncap = Q.ncap, nsel = Q.nsel;
+  const uint32_t smask = Q.stream_mask, sstream = Q.st_stream, topt = Q.tail_opt;
+  const uint64_t sbit = Q.st_bit, smin = Q.st_min, smax = Q.st_max;
+  const int64_t within = Q.within;
+  const bool every = Q.every != 0;
+  int cst[kMqMaxCaps], clast[kMqMaxCaps], csrc[kMqMaxCaps];
+#pragma unroll
+  for (int x = 0; x < kMqMaxCaps; ++x) {
+    cst[x] = x < ncap ? Q.cap_state[x] : -1;
+    clast[x] = Q.cap_last[x];
+    csrc[x] = Q.cap_src[x];
+  }
   uint64_t hdr = 0, sts = 0, cap[kMqMaxCaps];
 #pragma unroll
   for (int i = 0; i < kMqMaxCaps; ++i) cap[i] = 0;
@@ -251,16 +312,16 @@ __device__ uint32_t mq_seq(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
       sts = S[ks];
 #pragma unroll
       for (int i = 0; i < kMqMaxCaps; ++i)
-        if (i < Q.ncap) cap[i] = S[(int64_t)(2 + i) * ks];
+        if (i < ncap) cap[i] = S[(int64_t)(2 + i) * ks];
     }
   }
   bool live = (hdr & 1u) != 0, started = (hdr & 2u) != 0;
   int j = (int)((hdr >> 8) & 0xffu);
   uint32_t cnt = (uint32_t)(hdr >> 16);
   uint32_t rows = 0;
-  auto stream_of = [&](int s) { return (int)((Q.st_stream >> (3 * s)) & 7u); };
-  auto min_of = [&](int s) { return (uint32_t)((Q.st_min >> (8 * s)) & 0xffu); };
-  auto max_of = [&](int s) { return (uint32_t)((Q.st_max >> (8 * s)) & 0xffu); };
+  auto stream_of = [&](int s) { return (int)((sstream >> (3 * s)) & 7u); };
+  auto min_of = [&](int s) { return (uint32_t)((smin >> (8 * s)) & 0xffu); };
+  auto max_of = [&](int s) { return (uint32_t)((smax >> (8 * s)) & 0xffu); };
   for (uint32_t i = 0; i < maxlen; ++i) {
     bool em = false;
     int r = 0;
@@ -269,23 +330,23 @@ __device__ uint32_t mq_seq(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
       r = L.sorted[c.r0 + i];
       const uint64_t w0 = L.w0[r], w1 = L.w1[r];
       const int st = mq_stream(w0);
-      if ((Q.stream_mask >> st) & 1u) {
+      if ((smask >> st) & 1u) {
         ts = c.ts_base + (int64_t)(uint32_t)w0;
-        auto cond = [&](int s) { return ((w1 >> ((Q.st_bit >> (6 * s)) & 63u)) & 1ull) != 0; };
+        auto cond = [&](int s) { return ((w1 >> ((sbit >> (6 * s)) & 63u)) & 1ull) != 0; };
         auto collect = [&](int s, bool first) {
 #pragma unroll
           for (int x = 0; x < kMqMaxCaps; ++x)
-            if (x < Q.ncap && Q.cap_state[x] == s && (Q.cap_last[x] || first)) cap[x] = mq_src(c, Q.cap_src[x], r, ts);
+            if (cst[x] == s && (clast[x] || first)) cap[x] = mq_src(L, c, csrc[x], r, ts);
         };
         auto settle = [&]() {
-          if (cnt >= min_of(j) && ((Q.tail_opt >> j) & 1u)) {
+          if (cnt >= min_of(j) && ((topt >> j) & 1u)) {
             em = true;
             live = j == N - 1 && (max_of(j) == 0xffu || cnt < max_of(j));
           }
         };
-        if (live && Q.within >= 0) {
+        if (live && within >= 0) {
           const int64_t d = ts - (int64_t)sts;
-          if ((d < 0 ? -d : d) > Q.within) live = false;   // expired: dropped
+          if ((d < 0 ? -d : d) > within) live = false;   // expired: dropped
         }
         if (live) {
           bool adv = false;
@@ -313,7 +374,7 @@ __device__ uint32_t mq_seq(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
           }
           if (!adv) live = false;   // strict contiguity: discarded
         }
-        if (stream_of(0) == st && (Q.every || !started) && cond(0)) {
+        if (stream_of(0) == st && (every || !started) && cond(0)) {
           started = true;
           live = true;
           j = 0;
@@ -331,19 +392,16 @@ __device__ uint32_t mq_seq(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
       if (em) {
         const unsigned long long p = pos + (unsigned long long)__popcll(m & lanemask_lt());
         if ((int64_t)p < Q.out_cap) {
-          for (int x = 0; x < Q.nsel; ++x) {
-            const int src = Q.sel_src[x];
-            uint64_t v = (uint64_t)c.keyv;
-#pragma unroll
-            for (int y = 0; y < kMqMaxCaps; ++y)
-              if (src == SRC_CAP + y) v = cap[y];
-            store_col(Q.out_col[x], Q.sel_type[x], (int64_t)p, v);
-          }
           const uint32_t row = mq_row(L.w0[r]);
-          Q.out_ts[p] = ts;
-          Q.out_seq[p] = c.a->in_seq ? c.a->in_seq[row] : c.seq_base + row;
+          uint64_t vals[9];
+          vals[0] = (uint64_t)c.keyv;
+#pragma unroll
+          for (int y = 0; y < kMqMaxCaps; ++y) vals[1 + y] = cap[y];
+#pragma unroll
+          for (int y = 5; y < 9; ++y) vals[y] = 0;
+          mq_store_row(Q, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
         } else {
-          set_err(c.a->err, ERR_OUT_CAP);
+          set_err(c.err, ERR_OUT_CAP);
         }
       }
       pos += (unsigned long long)__popcll(m);
@@ -356,7 +414,7 @@ __device__ uint32_t mq_seq(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
       S[ks] = sts;
 #pragma unroll
       for (int i = 0; i < kMqMaxCaps; ++i)
-        if (i < Q.ncap) S[(int64_t)(2 + i) * ks] = cap[i];
+        if (i < ncap) S[(int64_t)(2 + i) * ks] = cap[i];
     }
   }
   return rows;
@@ -380,14 +438,28 @@ __device__ __forceinline__ bool mq_less(uint64_t a, uint64_t b, int t) {
   }
 }
 
-// One group-by aggregation over the 64 keys of a block (lane = group):
-// running values in arrival order (oracle/mq_oracle.c agg_event; sum over
-// int / long wraps in 64 bits, sum / avg over float / double accumulate in
-// double, min / max compare in the argument type), having on one output item.
+// One group-by aggregation over a block of 64 keys (lane = group): running
+// values in arrival order (oracle/mq_oracle.c agg_event; sum over int / long
+// wraps in 64 bits, sum / avg over float / double accumulate in double,
+// min / max compare in the argument type), having on one output item.
 template <bool kEmit, int NC>
-__device__ uint32_t mq_agg(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, int64_t ks, uint32_t maxlen,
-                           unsigned long long pos) {
-  const MqLds<NC>& L = *c.L;
+__device__ __forceinline__ uint32_t mq_agg(const MqLds<NC>& L, const MqCtx<NC>& c, CMqQuery& Q, uint64_t* S,
+                                           int64_t ks, uint32_t maxlen, unsigned long long pos) {
+  // the descriptor, decoded once (uniform: scalar registers)
+  const int in_st = Q.in_stream, fbit = Q.filter_bit, nagg = Q.nagg, nsel = Q.nsel;
+  int fn[kMqMaxAggs], at[kMqMaxAggs], asrc[kMqMaxAggs];
+  bool lsum[kMqMaxAggs];
+#pragma unroll
+  for (int y = 0; y < kMqMaxAggs; ++y) {
+    fn[y] = y < nagg ? Q.agg_fn[y] : AGG_COUNT;
+    at[y] = Q.agg_arg_type[y];
+    asrc[y] = Q.agg_src[y];
+    lsum[y] = Q.agg_out_type[y] == T_LONG;
+  }
+  const int hitem = Q.hav_item, hvi = Q.hav_vi;
+  const int htype = hitem >= 0 ? Q.sel_type[hitem] : 0;
+  const int hcop = Q.hav_cop, hctype = Q.hav_ctype;
+  const uint64_t hconst = Q.hav_cconst;
   uint64_t cnt = 0, acc[kMqMaxAggs];
 #pragma unroll
   for (int i = 0; i < kMqMaxAggs; ++i) acc[i] = 0;
@@ -395,17 +467,18 @@ __device__ uint32_t mq_agg(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
     cnt = S[0];
 #pragma unroll
     for (int i = 0; i < kMqMaxAggs; ++i)
-      if (i < Q.nagg) acc[i] = S[(int64_t)(1 + i) * ks];
+      if (i < nagg) acc[i] = S[(int64_t)(1 + i) * ks];
   }
-  auto aggval = [&](int i) -> uint64_t {
-    uint64_t x = 0;
+  // the row's value slots after the current event (MqQuery::sel_vi)
+  auto fill = [&](uint64_t (&vals)[9], int r, int64_t ts) {
+    vals[0] = (uint64_t)c.keyv;
 #pragma unroll
     for (int y = 0; y < kMqMaxAggs; ++y)
-      if (y == i) x = acc[y];
-    const int fn = Q.agg_fn[i];
-    if (fn == AGG_COUNT) return cnt;
-    if (fn == AGG_AVG) return from_f64(as_f64(x) / (double)(int64_t)cnt);
-    return x;
+      vals[1 + y] = fn[y] == AGG_COUNT ? cnt
+                    : fn[y] == AGG_AVG ? from_f64(as_f64(acc[y]) / (double)(int64_t)cnt)
+                                       : acc[y];
+#pragma unroll
+    for (int w = 0; w < kMqMaxCarry; ++w) vals[5 + w] = mq_src(L, c, w, r, ts);
   };
   uint32_t rows = 0;
   for (uint32_t i = 0; i < maxlen; ++i) {
@@ -415,35 +488,29 @@ __device__ uint32_t mq_agg(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
     if (i < c.len) {
       r = L.sorted[c.r0 + i];
       const uint64_t w0 = L.w0[r], w1 = L.w1[r];
-      if (mq_stream(w0) == Q.in_stream && ((w1 >> Q.filter_bit) & 1ull)) {
+      if (mq_stream(w0) == in_st && ((w1 >> fbit) & 1ull)) {
         ts = c.ts_base + (int64_t)(uint32_t)w0;
         const bool first = cnt == 0;
         cnt += 1;
 #pragma unroll
         for (int y = 0; y < kMqMaxAggs; ++y) {
-          if (y >= Q.nagg) break;
-          const int fn = Q.agg_fn[y];
-          if (fn == AGG_COUNT) continue;
-          const int at = Q.agg_arg_type[y];
-          const uint64_t v = mq_src(c, Q.agg_src[y], r, ts);
-          if (fn == AGG_SUM) {
-            acc[y] = Q.agg_out_type[y] == T_LONG ? acc[y] + v : from_f64(as_f64(acc[y]) + mq_as_double(v, at));
-          } else if (fn == AGG_AVG) {
-            acc[y] = from_f64(as_f64(acc[y]) + mq_as_double(v, at));
-          } else if (fn == AGG_MIN) {
-            if (first || mq_less(v, acc[y], at)) acc[y] = v;
+          if (fn[y] == AGG_COUNT) continue;   // (also every y >= nagg)
+          const uint64_t v = mq_src(L, c, asrc[y], r, ts);
+          if (fn[y] == AGG_SUM) {
+            acc[y] = lsum[y] ? acc[y] + v : from_f64(as_f64(acc[y]) + mq_as_double(v, at[y]));
+          } else if (fn[y] == AGG_AVG) {
+            acc[y] = from_f64(as_f64(acc[y]) + mq_as_double(v, at[y]));
+          } else if (fn[y] == AGG_MIN) {
+            if (first || mq_less(v, acc[y], at[y])) acc[y] = v;
           } else {
-            if (first || mq_less(acc[y], v, at)) acc[y] = v;
+            if (first || mq_less(acc[y], v, at[y])) acc[y] = v;
           }
         }
         em = true;
-        if (Q.hav_item >= 0) {
-          const int src = Q.sel_src[Q.hav_item];
-          uint64_t v = (uint64_t)c.keyv;
-          if (src >= SRC_AGG && src < SRC_AGG + kMaxAggs) v = aggval(src - SRC_AGG);
-          else if (src >= SRC_REC && src < SRC_REC + kMqMaxCarry) v = mq_src(c, src - SRC_REC, r, ts);
-          v = vm_convert(v, Q.sel_type[Q.hav_item], Q.hav_ctype);
-          em = vm_compare(Q.hav_cop, Q.hav_ctype, v, Q.hav_cconst);
+        if (hitem >= 0) {
+          uint64_t vals[9];
+          fill(vals, r, ts);
+          em = vm_compare(hcop, hctype, vm_convert(vals[hvi], htype, hctype), hconst);
         }
       }
     }
@@ -452,18 +519,12 @@ __device__ uint32_t mq_agg(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
       if (em) {
         const unsigned long long p = pos + (unsigned long long)__popcll(m & lanemask_lt());
         if ((int64_t)p < Q.out_cap) {
-          for (int x = 0; x < Q.nsel; ++x) {
-            const int src = Q.sel_src[x];
-            uint64_t v = (uint64_t)c.keyv;
-            if (src >= SRC_AGG && src < SRC_AGG + kMaxAggs) v = aggval(src - SRC_AGG);
-            else if (src >= SRC_REC && src < SRC_REC + kMqMaxCarry) v = mq_src(c, src - SRC_REC, r, ts);
-            store_col(Q.out_col[x], Q.sel_type[x], (int64_t)p, v);
-          }
           const uint32_t row = mq_row(L.w0[r]);
-          Q.out_ts[p] = ts;
-          Q.out_seq[p] = c.a->in_seq ? c.a->in_seq[row] : c.seq_base + row;
+          uint64_t vals[9];
+          fill(vals, r, ts);
+          mq_store_row(Q, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
         } else {
-          set_err(c.a->err, ERR_OUT_CAP);
+          set_err(c.err, ERR_OUT_CAP);
         }
       }
       pos += (unsigned long long)__popcll(m);
@@ -474,7 +535,7 @@ __device__ uint32_t mq_agg(const MqCtx<NC>& c, const MqQuery& Q, uint64_t* S, in
     S[0] = cnt;
 #pragma unroll
     for (int i = 0; i < kMqMaxAggs; ++i)
-      if (i < Q.nagg) S[(int64_t)(1 + i) * ks] = acc[i];
+      if (i < nagg) S[(int64_t)(1 + i) * ks] = acc[i];
   }
   return rows;
 }
@@ -497,6 +558,8 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
   const int RW = 2 + NC;
   const int64_t ks = a.kstride;
   const int64_t ts_base = a.chunk_base[0], seq_base = a.chunk_base[1];
+  CMqQuery* qc = (CMqQuery*)a.q;
+  const MqCtx<NC> c0{ts_base, seq_base, 0, 0, 0, a.lmap[0], a.lmap[1], a.lmap[2], a.lmap[3], a.in_seq, a.err};
   // this bucket's segment of every tile -> exclusive prefix over tiles
   {
     constexpr int MAXPER = kMqMaxTiles / NT;
@@ -547,6 +610,7 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       L.nwin = 0;
     }
     for (int k = tid; k <= kpb; k += NT) L.kstart[k] = 0;
+    for (int k = tid; k < 257; k += NT) L.lhist[k] = 0;
     lds_barrier();
     const int t1 = L.wt1;
     const bool split = t1 < 0;
@@ -626,9 +690,26 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
         L.sorted[j] = v;
       }
     }
+    // keys by descending run length: a wave's loop runs to the longest run
+    // of its 64 keys, so blocks of alike runs keep the lanes busy
+    auto bin_of = [&](int k) {
+      const uint32_t len = L.kstart[k + 1] - L.kstart[k];
+      return 255u - (len < 255u ? len : 255u);
+    };
+    for (int k = tid; k < kpb; k += NT) atomicAdd(&L.lhist[bin_of(k)], 1u);
+    lds_barrier();
+    {
+      const uint32_t c = tid < 256 ? L.lhist[tid] : 0u;
+      uint32_t tot;
+      const uint32_t off = bscan<NT>(c, L.scratch, &tot);
+      if (tid < 256) L.lhist[tid] = off;
+    }
+    lds_barrier();
+    for (int k = tid; k < kpb; k += NT) L.korder[atomicAdd(&L.lhist[bin_of(k)], 1u)] = (uint16_t)k;
+    lds_barrier();
     // longest run per 64-key block (the wave loops' trip count)
     for (int b = wave; b < nblk; b += NWV) {
-      const int k = b * 64 + lane;
+      const int k = b * 64 + lane < kpb ? L.korder[b * 64 + lane] : kpb;
       uint32_t len = k < kpb ? L.kstart[k + 1] - L.kstart[k] : 0u;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
@@ -641,20 +722,22 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
     const int nitems = a.nq * nblk;
     // pass 1: rows per (query, block)
     for (int it = wave; it < nitems; it += NWV) {
-      const int q = it / nblk, b = it - q * nblk;
+      const int q = __builtin_amdgcn_readfirstlane(it / nblk);
+      const int b = __builtin_amdgcn_readfirstlane(it - q * nblk);
       const uint32_t maxlen = L.bmax[b];
       uint32_t rows = 0;
       if (maxlen) {
-        const MqQuery& Q = a.q[q];
-        const int k = b * 64 + lane;
-        MqCtx<NC> c{&L, &a, ts_base, seq_base, 0, 0, 0};
+        CMqQuery& Q = qc[q];
+        const int k = b * 64 + lane < kpb ? L.korder[b * 64 + lane] : kpb;
+        MqCtx<NC> c = c0;
         if (k < kpb) {
           c.r0 = L.kstart[k];
           c.len = L.kstart[k + 1] - c.r0;
+          c.keyv = ((((int64_t)k << lg) | bucket) * a.key_stride) + a.key_offset;
         }
         uint64_t* S = a.state + Q.st_off * ks + (int64_t)bucket * kpb + (k < kpb ? k : 0);
-        rows = Q.kind == MQ_SEQ ? mq_seq<false, NC>(c, Q, S, ks, maxlen, 0)
-                                : mq_agg<false, NC>(c, Q, S, ks, maxlen, 0);
+        rows = Q.kind == MQ_SEQ ? mq_seq<false, NC>(L, c, Q, S, ks, maxlen, 0)
+                                : mq_agg<false, NC>(L, c, Q, S, ks, maxlen, 0);
       }
       if (lane == 0) L.qoff[q * nblk + b] = rows;
     }
@@ -667,27 +750,27 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
         L.qoff[tid * nblk + b] = s;
         s += c;
       }
-      L.qbase[tid] = s ? atomicAdd(a.q[tid].out_count, (unsigned long long)s) : 0ull;
+      L.qbase[tid] = s ? atomicAdd(qc[tid].out_count, (unsigned long long)s) : 0ull;
     }
     lds_barrier();
     // pass 2: rows + state commit
     for (int it = wave; it < nitems; it += NWV) {
-      const int q = it / nblk, b = it - q * nblk;
+      const int q = __builtin_amdgcn_readfirstlane(it / nblk);
+      const int b = __builtin_amdgcn_readfirstlane(it - q * nblk);
       const uint32_t maxlen = L.bmax[b];
       if (!maxlen) continue;
-      const MqQuery& Q = a.q[q];
-      const int k = b * 64 + lane;
-      MqCtx<NC> c{&L, &a, ts_base, seq_base, 0, 0, 0};
+      CMqQuery& Q = qc[q];
+      const int k = b * 64 + lane < kpb ? L.korder[b * 64 + lane] : kpb;
+      MqCtx<NC> c = c0;
       if (k < kpb) {
         c.r0 = L.kstart[k];
         c.len = L.kstart[k + 1] - c.r0;
-        const int64_t kl = ((int64_t)k << lg) | bucket;
-        c.keyv = kl * a.key_stride + a.key_offset;
+        c.keyv = ((((int64_t)k << lg) | bucket) * a.key_stride) + a.key_offset;
       }
       uint64_t* S = a.state + Q.st_off * ks + (int64_t)bucket * kpb + (k < kpb ? k : 0);
       const unsigned long long pos = L.qbase[q] + L.qoff[q * nblk + b];
-      if (Q.kind == MQ_SEQ) mq_seq<true, NC>(c, Q, S, ks, maxlen, pos);
-      else mq_agg<true, NC>(c, Q, S, ks, maxlen, pos);
+      if (Q.kind == MQ_SEQ) mq_seq<true, NC>(L, c, Q, S, ks, maxlen, pos);
+      else mq_agg<true, NC>(L, c, Q, S, ks, maxlen, pos);
     }
     // the next window re-reads state this one wrote and reuses the LDS arrays
     if (t0 < ntiles) __syncthreads();

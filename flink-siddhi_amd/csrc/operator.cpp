@@ -156,7 +156,12 @@ cep_app* cep_operator_plan(cep_operator* o, const char* plan_id) {
 int cep_operator_send(cep_operator* o, const char* stream_id, const cep_batch* b, int* plans_sent) {
   if (!o || !stream_id || !b) return CEP_E_ARG;
   if (b->stream) return op_fail(o, CEP_E_ARG, "cep_operator_send takes single-stream batches (stream == NULL)");
-  int sent = 0;
+  // Every enabled plan gets the batch on its own, as AddRouteOperator sends
+  // to each plan (router/AddRouteOperator.java:54-175): a plan that fails
+  // does not keep the later ones from their input; the first failure (with
+  // its plan id) is returned after the loop.
+  int sent = 0, first_rc = CEP_OK;
+  std::string first_msg;
   for (auto& kv : o->plans) {
     auto& p = kv.second;
     if (!p.enabled) continue;
@@ -165,10 +170,17 @@ int cep_operator_send(cep_operator* o, const char* stream_id, const cep_batch* b
     bb.input = cep_input(p.app, stream_id);
     if (bb.input < 0) continue;
     const int rc = cep_send_batch(p.app, &bb);
-    if (rc) return op_fail(o, rc, kv.first + ": " + cep_last_error(p.app));
+    if (rc) {
+      if (first_rc == CEP_OK) {
+        first_rc = rc;
+        first_msg = kv.first + ": " + cep_last_error(p.app);
+      }
+      continue;
+    }
     ++sent;
   }
   if (plans_sent) *plans_sent = sent;
+  if (first_rc != CEP_OK) return op_fail(o, first_rc, first_msg);
   return CEP_OK;
 }
 

@@ -195,7 +195,8 @@ class SiddhiAppRuntime:
         """processWatermark (AbstractSiddhiOperator.java:238-247): buffered rows
         with ts <= mark reach the engine in (ts, arrival) order; later rows
         stay buffered.  A row older than one already released (a late event)
-        is dropped and counted in stats().late_events."""
+        is dropped and counted in stats().late_events; with the runtime
+        option late_policy=1 the call then raises (after the release)."""
         self._check(self._lib.cep_watermark(self._h, int(mark)))
 
     def buffered(self) -> int:

@@ -101,7 +101,14 @@ typedef struct cep_options {
   int32_t sparse_keys;     /* 1: partition values are any int / long (a device hash map
                               assigns up to key_capacity dense slots; values come back
                               unchanged in `select s1.k`); 0: ints in [0, key_capacity) */
-  int32_t reserved[5];
+  int32_t late_policy;     /* event time (cep_watermark): a row older than rows an earlier
+                              watermark released is a late event.  0: dropped and counted in
+                              cep_stats.late_events (default); 1: dropped, and cep_watermark
+                              returns CEP_E_ARG after releasing the on-time rows.  The
+                              reference hands late rows to Siddhi out of order
+                              (AbstractSiddhiOperator.java:238-245); `within` and sequences
+                              need event-time order, so the engine never processes them. */
+  int32_t reserved[4];
 } cep_options;
 
 /* Fill *opt with defaults. */
@@ -308,7 +315,10 @@ int cep_operator_enable(cep_operator* op, const char* plan_id, int enabled);
 /* The plan's runtime (callbacks, stats, snapshot), or NULL. */
 cep_app* cep_operator_plan(cep_operator* op, const char* plan_id);
 /* A single-stream batch (batch->stream == NULL) of stream_id to every enabled
- * plan that reads it (router/AddRouteOperator.java:65-96); *plans_sent = fan-out. */
+ * plan that reads it (router/AddRouteOperator.java:65-96); *plans_sent = plans
+ * that took it.  A plan that fails does not stop the others: every plan gets
+ * the batch, and the first failure (message prefixed with its plan id) is
+ * returned after the loop. */
 int cep_operator_send(cep_operator* op, const char* stream_id, const cep_batch* batch, int* plans_sent);
 int cep_operator_flush(cep_operator* op);
 /* Shared string dictionary of the operator's plans (STRING columns sent with

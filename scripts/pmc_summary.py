@@ -14,7 +14,8 @@ import sys
 
 
 def short(name):
-    for k in ("k_cfpart", "k_cfwalk", "k_partition", "k_walk", "k_filter", "k_generate", "k_route"):
+    for k in ("k_cfpart", "k_cfwalk", "k_mqpart", "k_mqwalk", "k_partition", "k_walk", "k_filter", "k_generate",
+              "k_route"):
         if k in name:
             return k
     return None

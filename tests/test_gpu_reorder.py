@@ -129,6 +129,30 @@ def test_late_event_is_dropped():
     assert_same_rows(got, want, "late row dropped")
 
 
+def test_late_policy_reports_late_events():
+    """late_policy=1: the on-time rows are still released, the late row is
+    dropped, and the watermark call raises so a caller relying on the
+    reference's hand-over of late rows (AbstractSiddhiOperator.java:238-245)
+    notices."""
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, late_policy=1)
+    n = 50
+    ts = np.arange(1000, 1000 + n, dtype=np.int64)
+    z = np.zeros(n, dtype=np.int32)
+    p = np.full(n, 0.75)
+    st = np.zeros(n, dtype=np.uint8)
+    rt.process_elements("A", ts, [z, ts, z, p], streams=st)
+    rt.process_watermark(1020)
+    late = np.array([1005], dtype=np.int64)
+    rt.process_elements("A", late, [z[:1], late, z[:1], p[:1]], streams=st[:1])
+    with pytest.raises(ValueError, match="late"):
+        rt.process_watermark(1030)
+    assert rt.stats().late_events == 1
+    assert rt.buffered() == n - 31
+    rt.process_watermark(2000)     # no late rows: fine
+    assert rt.buffered() == 0
+    rt.shutdown()
+
+
 def test_reordered_filter_matches_oracle():
     plan = workload.FILTER_PLAN
     n = 30000
