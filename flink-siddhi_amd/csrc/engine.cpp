@@ -173,6 +173,9 @@ struct MqRT {
   bool used[2] = {false, false};
   int cur = 0;
   bool dq_dirty = true;
+  std::vector<int> classes_kind, classes_n;   // shape classes in descriptor order (MqUnit kinds, sizes)
+  std::vector<MqUnit> units;
+  DevBuf du;
 };
 
 struct TimedLaunch {
@@ -467,65 +470,205 @@ std::vector<int> mq_pref_cols(const MqRT& g) {
   return v;
 }
 
+// A shape class of one group's queries (walk unit kinds, kernels.h MqUnit).
+struct MqClassB {
+  int kind = MQU_SEQ;
+  std::string sig;
+  int key_col = -1, layout = -1;
+  std::vector<int> qs;
+  std::vector<MqNeeds> nds;
+};
+
+// Shape signature: queries with equal signatures run as one walk unit
+// (sequence classes advance bit-parallel, aggregations share the decode).
+std::string mq_signature(const cep_app* a, const Query& q, const MqNeeds& nd, int* kind) {
+  const CompiledApp& app = a->app;
+  std::string sg = std::to_string(nd.key_col) + "/" + std::to_string(nd.layout) + "|";
+  auto add = [&](int64_t v) { sg += std::to_string(v) + ","; };
+  const auto& od = app.outputs[app.output_index(q.out_stream)];
+  for (auto& at : od.attrs) add(at.type);
+  sg += "|";
+  for (auto& it : q.select) add(it.src >= SRC_REC && it.src < SRC_REC + (int)q.rec_cols_a.size()
+                                    ? 1000 + q.rec_cols_a[it.src - SRC_REC] : it.src);
+  sg += "|";
+  if (q.kind == Q_AGG) {
+    *kind = MQU_AGG;
+    add(q.in_stream);
+    for (auto& ag : q.aggs) {
+      add(ag.fn);
+      add(ag.word >= 0 ? q.rec_cols_a[ag.word] : -1);
+      add(ag.arg_type);
+      add(ag.out_type);
+    }
+    sg += "|";
+    add(q.having_item);
+    if (q.having_item >= 0) {
+      add(q.having_cop);
+      add(q.having_ctype);
+    }
+    return "A" + sg;
+  }
+  // sequences: bit-parallel when every state reads its own stream and counts
+  // "one" or "one or more" (optional states allowed)
+  bool bp = true;
+  const int n = (int)q.nstates.size();
+  for (int j = 0; j < n; ++j) {
+    const auto& st = q.nstates[j];
+    for (int k = 0; k < j; ++k) bp = bp && q.nstates[k].stream != st.stream;
+    bp = bp && st.min_count <= 1 && (st.max_count == 1 || st.max_count < 0);
+  }
+  *kind = bp ? MQU_SEQ_BP : MQU_SEQ;
+  add(q.every ? 1 : 0);
+  add(q.within);
+  for (auto& st : q.nstates) {
+    add(st.stream);
+    add(st.min_count);
+    add(st.max_count);
+  }
+  sg += "|";
+  for (auto& cp : q.ncaps) {
+    add(cp.state);
+    add(cp.index);
+    add(q.rec_cols_a[cp.word]);
+  }
+  return "S" + sg;
+}
+
+// Record bit of a run of conditions on stream s (query order), sharing an
+// identical run already placed; -1 when the stream's bits are used up.
+int mq_cond_run(MqRT& g, int s, const std::vector<TermList>& run, bool add) {
+  const int n = (int)run.size();
+  for (int i = 0; i + n <= g.ncond[s]; ++i) {
+    bool same = true;
+    for (int j = 0; j < n && same; ++j) same = same_terms(g.conds[s * kMqMaxCond + i + j].tl, run[j]);
+    if (same) return i;
+  }
+  if (g.ncond[s] + n > kMqMaxCond) return -1;
+  if (!add) return g.ncond[s];
+  const int at = g.ncond[s];
+  for (int j = 0; j < n; ++j) {
+    MqCond& mc = g.conds[s * kMqMaxCond + at + j];
+    std::memset(&mc, 0, sizeof(mc));
+    mc.tl = run[j];
+  }
+  g.ncond[s] += n;
+  return at;
+}
+
+// Place a class's conditions into group g (bit-parallel classes: one run per
+// state; others: one bit per distinct condition).  false: no room.
+bool mq_place_conds(const cep_app* a, MqRT& g, const MqClassB& c) {
+  const CompiledApp& app = a->app;
+  if (c.kind == MQU_SEQ_BP) {
+    const Query& q0 = app.queries[c.qs[0]];
+    for (size_t j = 0; j < q0.nstates.size(); ++j) {
+      std::vector<TermList> run;
+      bool any = false;
+      for (int qi : c.qs) {
+        run.push_back(app.queries[qi].nstates[j].terms);
+        any = any || app.queries[qi].nstates[j].terms.n > 0;
+      }
+      if (any && mq_cond_run(g, q0.nstates[j].stream, run, true) < 0) return false;
+    }
+    return true;
+  }
+  for (auto& nd : c.nds)
+    for (auto& cd : nd.conds)
+      if (cd.second.n > 0 && mq_cond_run(g, cd.first, {cd.second}, true) < 0) return false;
+  return true;
+}
+
 int build_mq_groups(cep_app* a) {
   const CompiledApp& app = a->app;
   a->in_mq.assign(app.queries.size(), 0);
   if (std::getenv("CEP_NO_MQ") || app.inputs.size() > 8) return CEP_OK;
-  std::vector<int> layouts;   // per group: a stream of its layout
+  // shape classes of the candidates, in plan order of their first query
+  std::vector<MqClassB> classes;
   for (size_t qi = 0; qi < app.queries.size(); ++qi) {
     MqNeeds nd;
     if (!mq_candidate(a, app.queries[qi], &nd)) continue;
-    int gi = -1;
-    for (size_t i = 0; i < a->mqs.size() && gi < 0; ++i) {
-      MqRT& g = a->mqs[i];
-      if ((int)g.qs.size() >= kMqMaxQ || g.key_col != nd.key_col || !same_layout(app, layouts[i], nd.layout))
-        continue;
-      // conditions, carried and prefetched columns still fit
-      int extra[8] = {0};
-      bool ok = true;
-      for (auto& c : nd.conds) {
-        const int b = mq_cond_bit(g, c.first, c.second, false);
-        if (b < 0) ok = false;
-        else if (b == g.ncond[c.first]) {
-          bool dup = false;   // the same new condition twice in this query
-          for (auto& d : nd.conds)
-            if (&d != &c && d.first == c.first && same_terms(d.second, c.second) && &d < &c) dup = true;
-          if (!dup) ++extra[c.first];
-        }
-      }
-      for (int s = 0; s < 8 && ok; ++s) ok = g.ncond[s] + extra[s] <= kMqMaxCond;
+    int kind;
+    const std::string sig = mq_signature(a, app.queries[qi], nd, &kind);
+    MqClassB* c = nullptr;
+    for (auto& x : classes)
+      if (x.sig == sig && x.kind != MQU_SEQ && (int)x.qs.size() < (x.kind == MQU_SEQ_BP ? kMqMaxCond : kMqMaxQ))
+        c = &x;
+    if (!c) {
+      classes.push_back(MqClassB());
+      c = &classes.back();
+      c->kind = kind;
+      c->sig = sig;
+      c->key_col = nd.key_col;
+      c->layout = nd.layout;
+    }
+    c->qs.push_back((int)qi);
+    c->nds.push_back(nd);
+  }
+  // classes into groups: a class joins the first group with room (queries,
+  // carried / prefetched columns, condition bits); a class too large for an
+  // empty group is halved
+  std::vector<int> layouts;   // per group: a stream of its layout
+  std::vector<std::vector<MqClassB>> gclasses;
+  for (size_t ci = 0; ci < classes.size(); ++ci) {
+    MqClassB c = classes[ci];
+    auto fits = [&](MqRT& g) {
       MqRT t;
       t.key_col = g.key_col;
       t.cond_cols = g.cond_cols;
       t.carry = g.carry;
-      for (int c : nd.cols) mq_index(t.cond_cols, c);
-      for (int c : nd.carry) mq_index(t.carry, c);
-      ok = ok && (int)t.carry.size() <= kMqMaxCarry && (int)mq_pref_cols(t).size() <= kPref;
-      if (ok) gi = (int)i;
-    }
+      t.conds = g.conds;
+      std::copy(g.ncond, g.ncond + 8, t.ncond);
+      for (auto& nd : c.nds) {
+        for (int x : nd.cols) mq_index(t.cond_cols, x);
+        for (int x : nd.carry) mq_index(t.carry, x);
+      }
+      if ((int)t.carry.size() > kMqMaxCarry || (int)mq_pref_cols(t).size() > kPref) return false;
+      if ((int)(g.qs.size() + c.qs.size()) > kMqMaxQ) return false;
+      if (!mq_place_conds(a, t, c)) return false;
+      g.cond_cols = t.cond_cols;
+      g.carry = t.carry;
+      g.conds = t.conds;
+      std::copy(t.ncond, t.ncond + 8, g.ncond);
+      return true;
+    };
+    int gi = -1;
+    for (size_t i = 0; i < a->mqs.size() && gi < 0; ++i)
+      if (a->mqs[i].key_col == c.key_col && same_layout(app, layouts[i], c.layout) && fits(a->mqs[i])) gi = (int)i;
     if (gi < 0) {
       MqRT g;
-      g.key_col = nd.key_col;
+      g.key_col = c.key_col;
       g.conds.resize(8 * kMqMaxCond);
-      for (int c : nd.cols) mq_index(g.cond_cols, c);
-      for (int c : nd.carry) mq_index(g.carry, c);
-      if ((int)g.carry.size() > kMqMaxCarry || (int)mq_pref_cols(g).size() > kPref) continue;
-      int per[8] = {0};
-      for (auto& c : nd.conds) per[c.first]++;
-      bool ok = true;
-      for (int s = 0; s < 8; ++s) ok = ok && per[s] <= kMqMaxCond;
-      if (!ok) continue;
+      if (!fits(g)) {
+        if (c.qs.size() > 1) {   // halve the class and place both halves
+          MqClassB h = c;
+          const size_t m = c.qs.size() / 2;
+          c.qs.resize(m);
+          c.nds.resize(m);
+          h.qs.erase(h.qs.begin(), h.qs.begin() + m);
+          h.nds.erase(h.nds.begin(), h.nds.begin() + m);
+          classes[ci] = c;
+          classes.insert(classes.begin() + ci + 1, h);
+          --ci;
+        }
+        continue;   // a single query that fits no group: general path
+      }
       a->mqs.push_back(std::move(g));
-      layouts.push_back(nd.layout);
+      layouts.push_back(c.layout);
+      gclasses.emplace_back();
       gi = (int)a->mqs.size() - 1;
     }
     MqRT& g = a->mqs[gi];
-    for (int c : nd.cols) mq_index(g.cond_cols, c);
-    for (int c : nd.carry) mq_index(g.carry, c);
-    for (auto& c : nd.conds) mq_cond_bit(g, c.first, c.second, true);
-    g.qs.push_back((int)qi);
-    a->in_mq[qi] = 1;
+    for (int qi : c.qs) {
+      g.qs.push_back(qi);
+      a->in_mq[qi] = 1;
+    }
+    gclasses[gi].push_back(c);
   }
+  for (size_t gi = 0; gi < a->mqs.size(); ++gi)
+    for (auto& c : gclasses[gi]) {
+      a->mqs[gi].classes_kind.push_back(c.kind);
+      a->mqs[gi].classes_n.push_back((int)c.qs.size());
+    }
   // device descriptors, state and arenas per group
   for (auto& g : a->mqs) {
     const int64_t K = a->opt.key_capacity;
@@ -548,8 +691,11 @@ int build_mq_groups(cep_app* a) {
     g.lg = lg;
     g.kpb = (int)kpb;
     g.kstride = kpb << lg;
-    // descriptors
+    // descriptors (class order), then the walk units
     int64_t off = 0;
+    std::vector<int> qkind;   // per descriptor: its class's unit kind
+    for (size_t ci = 0; ci < g.classes_kind.size(); ++ci)
+      for (int i = 0; i < g.classes_n[ci]; ++i) qkind.push_back(g.classes_kind[ci]);
     for (int qi : g.qs) {
       const Query& q = app.queries[qi];
       MqQuery d;
@@ -625,12 +771,69 @@ int build_mq_groups(cep_app* a) {
       d.hav_vi = d.hav_item >= 0 ? d.sel_vi[d.hav_item] : 0;
       g.stream_mask |= d.stream_mask;
       g.check_order = g.check_order || (d.kind == MQ_SEQ && d.within >= 0);
+      if (qkind[g.hq.size()] == MQU_SEQ_BP) d.nwords = 0;   // class state (unit)
       off += d.nwords;
       g.hq.push_back(d);
+    }
+    g.units.clear();
+    for (size_t ci = 0, q0 = 0; ci < g.classes_kind.size(); q0 += g.classes_n[ci], ++ci) {
+      const int n = g.classes_n[ci];
+      MqUnit u;
+      std::memset(&u, 0, sizeof(u));
+      u.kind = g.classes_kind[ci];
+      u.q0 = (int)q0;
+      if (u.kind == MQU_SEQ) {
+        for (int i = 0; i < n; ++i) {
+          u.q0 = (int)q0 + i;
+          u.nq = 1;
+          g.units.push_back(u);
+        }
+      } else if (u.kind == MQU_SEQ_BP) {
+        const Query& q = app.queries[g.qs[q0]];
+        const int N = (int)q.nstates.size();
+        u.nq = n;
+        u.st_off = off;
+        off += 4 + (int64_t)q.ncaps.size();   // live mask, started mask, state, start ts, captures
+        u.keep_last = q.nstates[N - 1].max_count < 0 ? 1 : 0;
+        for (int j = 0; j < N; ++j) {
+          const auto& st = q.nstates[j];
+          u.st_of_stream |= (uint32_t)(j + 1) << (4 * st.stream);
+          for (int t = 0; t < N; ++t) {
+            bool ok = (t == j && st.max_count < 0);
+            if (t > j) {
+              ok = true;
+              for (int k = j + 1; k < t; ++k) ok = ok && q.nstates[k].min_count == 0;
+            }
+            if (ok) u.allow |= 1ull << (j * 8 + t);
+          }
+          std::vector<TermList> run;
+          bool any = false;
+          for (int i = 0; i < n; ++i) {
+            run.push_back(app.queries[g.qs[q0 + i]].nstates[j].terms);
+            any = any || run.back().n > 0;
+          }
+          const uint64_t cb = any ? (uint64_t)mq_cond_run(g, st.stream, run, false) : 0xffull;
+          u.cbase |= cb << (8 * j);
+        }
+        for (int j = N; j < 8; ++j) u.cbase |= 0xffull << (8 * j);
+        g.units.push_back(u);
+      } else {
+        const Query& q = app.queries[g.qs[q0]];
+        int na = 0;
+        for (auto& ag : q.aggs) na += ag.fn != AGG_COUNT ? 1 : 0;
+        const int nu = na <= 1 ? 8 : na == 2 ? 4 : 2;   // k_mqwalk's mq_agg_unit widths
+        for (int i = 0; i < n; i += nu) {
+          u.q0 = (int)q0 + i;
+          u.nq = std::min(nu, n - i);
+          u.nu = nu;
+          g.units.push_back(u);
+        }
+      }
     }
     g.words = off;
     const int ntiles = (int)(g.chunk / kMqTile);
     bool ok = dev_ensure(&g.dq, g.hq.size() * sizeof(MqQuery), a->stream, false) &&
+              dev_ensure(&g.du, g.units.size() * sizeof(MqUnit), a->stream, false) &&
               dev_ensure(&g.dconds, g.conds.size() * sizeof(MqCond), a->stream, false) &&
               dev_ensure(&g.state, (size_t)g.words * g.kstride * 8, a->stream, false);
     for (int b = 0; b < 2 && ok; ++b)
@@ -648,6 +851,7 @@ int build_mq_groups(cep_app* a) {
         for (size_t sl = 0; sl < pc.size(); ++sl)
           if (pc[sl] == mc.tl.t[i].col) mc.slot[i] = (int32_t)sl;
     hipMemcpy(g.dconds.p, g.conds.data(), g.conds.size() * sizeof(MqCond), hipMemcpyHostToDevice);
+    hipMemcpy(g.du.p, g.units.data(), g.units.size() * sizeof(MqUnit), hipMemcpyHostToDevice);
   }
   return CEP_OK;
 }
@@ -1413,6 +1617,8 @@ int run_mq(cep_app* a, MqRT& g, const RowsArgs& rows_all) {
   pa.err = (unsigned int*)a->err.p;
   wa.q = (const MqQuery*)g.dq.p;
   wa.nq = (int)g.qs.size();
+  wa.units = (const MqUnit*)g.du.p;
+  wa.nunits = (int)g.units.size();
   wa.nphys = nphys;
   wa.buckets_log2 = g.lg;
   wa.kpb = g.kpb;
@@ -1421,6 +1627,7 @@ int run_mq(cep_app* a, MqRT& g, const RowsArgs& rows_all) {
   wa.state = (uint64_t*)g.state.p;
   wa.kstride = g.kstride;
   wa.err = pa.err;
+  if (a->stamps.p && (1 << g.lg) * 8 <= 2 * 4096 * 16) wa.stamps = (uint64_t*)a->stamps.p;
   // the side stream starts after everything already queued on the main one
   hipEventRecord(a->in_ready, a->stream);
   hipStreamWaitEvent(a->side, a->in_ready, 0);
@@ -1679,6 +1886,18 @@ void cep_destroy(cep_app* a) {
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, ps[i] / nt);
     std::fprintf(stderr, " span=%.0f\n", (double)(phi - plo));
   }
+  if (a->stamps.p && !a->mqs.empty()) {
+    // diagnostics: mean ticks per multi-query walk phase over the last launch's buckets
+    const int nb = 1 << a->mqs[0].lg;
+    std::vector<uint64_t> st((size_t)nb * 8);
+    hipMemcpy(st.data(), a->stamps.p, st.size() * 8, hipMemcpyDeviceToHost);
+    double sum[8] = {0};
+    for (int b = 0; b < nb; ++b)
+      for (int i = 1; i < 5; ++i)
+        if (st[(size_t)b * 8 + i] && st[(size_t)b * 8 + i - 1]) sum[i] += (double)(st[(size_t)b * 8 + i] - st[(size_t)b * 8 + i - 1]);
+    std::fprintf(stderr, "[cep stamps] mq walk ticks/bucket: gather=%.0f sort=%.0f count=%.0f emit=%.0f\n",
+                 sum[1] / nb, sum[2] / nb, sum[3] / nb, sum[4] / nb);
+  }
   harvest_timers(a);
   for (auto e : a->event_pool) hipEventDestroy(e);
   for (auto& o : a->outs) {
@@ -1710,7 +1929,7 @@ void cep_destroy(cep_app* a) {
     }
   }
   for (auto& g : a->mqs) {
-    for (DevBuf* b : {&g.dq, &g.dconds, &g.state}) dev_free(b);
+    for (DevBuf* b : {&g.dq, &g.du, &g.dconds, &g.state}) dev_free(b);
     for (int b = 0; b < 2; ++b) {
       dev_free(&g.recs[b]);
       dev_free(&g.toff[b]);

@@ -456,6 +456,30 @@ struct MqQuery {
   int64_t out_cap;
 };
 
+// Walk units: what one wave runs over a block of 64 keys.
+//   MQU_SEQ     one sequence query (general shape, its own partial per key);
+//   MQU_SEQ_BP  a class of sequence queries of one shape whose states read
+//               distinct streams and count at most "one or more": all of a
+//               key's live partials then share state, start and captures, so
+//               the class advances bit-parallel (a live mask per key, one bit
+//               per query; the per-state conditions of the class are a run of
+//               consecutive record bits in query order);
+//   MQU_AGG     up to 8 aggregations of one shape (stream, functions,
+//               arguments, select / having layout), each query's running
+//               values in the lane's registers: the record is decoded once.
+enum : int32_t { MQU_SEQ = 0, MQU_SEQ_BP = 1, MQU_AGG = 2 };
+struct MqUnit {
+  int32_t kind;
+  int32_t q0, nq;                 // descriptors [q0, q0 + nq)
+  int32_t nu;                     // MQU_AGG: queries held in registers (template width)
+  // MQU_SEQ_BP: class state words at st_off (live mask, started mask, state, start ts, captures)
+  int64_t st_off;
+  uint32_t st_of_stream;          // 4 bits per input handle: state + 1 (0: the class does not read it)
+  uint64_t allow;                 // bit j * 8 + s: a partial in state j moves to (or stays in) state s
+  uint64_t cbase;                 // 8 bits per state: first record bit of the class's condition run (0xff: none)
+  uint32_t keep_last;             // the last state collects more (unbounded) after emitting
+};
+
 struct MqPartArgs {
   RowsArgs rows;
   PrefPlan pref;                  // prefetched columns: key, condition columns, carried columns
@@ -480,6 +504,8 @@ struct MqPartArgs {
 struct MqWalkArgs {
   const MqQuery* q;
   int32_t nq;
+  const MqUnit* units;
+  int32_t nunits;
   int32_t nphys;
   int32_t lmap[kMqMaxCarry];      // logical carried word -> physical word, -1: the event ts
   const uint64_t* recs;
@@ -492,6 +518,7 @@ struct MqWalkArgs {
   const int64_t* in_seq;          // per-row arrival numbers of the chunk (row shuffle), or nullptr
   uint64_t* state;                // per-query SoA state words over the bucket-major key index
   int64_t kstride;
+  uint64_t* stamps;               // diagnostics (CEP_STAMPS=1): per bucket 8 s_memtime stamps
   unsigned int* err;
 };
 

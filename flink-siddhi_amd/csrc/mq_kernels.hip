@@ -30,6 +30,8 @@
 // (engine.cpp checks the shape).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dev_common.h"
 #include "kernels.h"
 #include "vm.h"
@@ -43,6 +45,27 @@ __device__ __forceinline__ int mq_stream(uint64_t w0) { return (int)(w0 >> 57) &
 __device__ __forceinline__ uint32_t mq_key(uint64_t w1) { return (uint32_t)(w1 >> 48); }
 
 }  // namespace
+
+// Conditions are read through the constant address space: scalar loads into
+// a local copy (a generic pointer makes every term field a vector load).
+typedef __attribute__((address_space(4))) const MqCond CMqCond;
+
+__device__ __forceinline__ void mq_load_cond(CMqCond& c, TermList* tl, int32_t (&slot)[kMaxTerms]) {
+  tl->n = c.tl.n;
+  tl->any = c.tl.any;
+#pragma unroll
+  for (int i = 0; i < kMaxTerms; ++i) {
+    tl->t[i].col = c.tl.t[i].col;
+    tl->t[i].coltype = c.tl.t[i].coltype;
+    tl->t[i].aop = c.tl.t[i].aop;
+    tl->t[i].atype = c.tl.t[i].atype;
+    tl->t[i].aconst = c.tl.t[i].aconst;
+    tl->t[i].cop = c.tl.t[i].cop;
+    tl->t[i].ctype = c.tl.t[i].ctype;
+    tl->t[i].cconst = c.tl.t[i].cconst;
+    slot[i] = c.slot[i];
+  }
+}
 
 // ============================================================== k_mqpart ==
 // Two passes over the tile's rows inside one workgroup, so a tile can be
@@ -168,9 +191,12 @@ __global__ __launch_bounds__(kMqPartThreads, 1) void k_mqpart(MqPartArgs a) {
         for (int e = 0; e < EB; ++e) is_s |= (((vg >> e) & 1u) && sb[e] == (uint32_t)s ? 1u : 0u) << e;
         const int nc = a.ncond[s];
         if (!__ballot(is_s != 0) || nc == 0) continue;
-        const MqCond* cs = a.conds + s * kMqMaxCond;
+        CMqCond* cs = (CMqCond*)a.conds + s * kMqMaxCond;
         for (int c = 0; c < nc; ++c) {
-          const uint32_t bits = eval_terms_regs<EB, NP>(cs[c].tl, cs[c].slot, a.rows.cols, pv) & is_s;
+          TermList tl;
+          int32_t slot[kMaxTerms];
+          mq_load_cond(cs[c], &tl, slot);
+          const uint32_t bits = eval_terms_regs<EB, NP>(tl, slot, a.rows.cols, pv) & is_s;
 #pragma unroll
           for (int e = 0; e < EB; ++e) mask[e] |= (uint64_t)((bits >> e) & 1u) << c;
         }
@@ -211,6 +237,17 @@ namespace {
 
 constexpr int mq_window(int nc) { return nc <= 1 ? kMqWindow : (nc == 2 ? 3072 : 2048); }
 
+// Per-query data the step loops read, staged in LDS at kernel start: read
+// where used (a scalar copy of every query's output pointers would not fit
+// the scalar register file).
+struct MqHot {
+  uint64_t col[kMqMaxSel];
+  uint64_t ts, seq, hconst;
+  int64_t cap;
+  uint64_t viw;                           // 8 bits per select item: value slot | width << 4
+  uint32_t fbit, pad;
+};
+
 // A window's records in LDS (structure of arrays).
 template <int NC>
 struct MqLds {
@@ -225,6 +262,8 @@ struct MqLds {
   uint32_t lhist[257];                   // run-length bins (descending), then their cursors
   uint32_t qoff[kMqMaxQ * (kMqMaxKpb / 64)];   // per (query, block): rows, then first row
   unsigned long long qbase[kMqMaxQ];
+  unsigned long long wcur[kMqWalkThreads / 64][kMqMaxQ];   // per wave: a unit's row counts / output cursors
+  MqHot hot[kMqMaxQ];                    // per query: what the step loops read (outputs, filter, having constant)
   uint32_t seg[kMqMaxTiles + 1];         // exclusive prefix of the bucket's tile segments
   uint16_t lo[kMqMaxTiles];              // segment start inside each tile
   uint32_t scratch[kMqWalkThreads / 64 + 1];
@@ -268,28 +307,31 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // Output row p of a query from its value slots (MqQuery::sel_vi: 0 the key,
 // 1 + i capture / aggregate i, 5 + w carried word w): one uniform-indexed
 // register read and one store per column, unrolled.
-__device__ __forceinline__ void mq_store_row(CMqQuery& Q, int nsel, unsigned long long p, const uint64_t (&vals)[9],
+__device__ __forceinline__ void mq_store_row(const MqHot& H, int nsel, unsigned long long p, const uint64_t (&vals)[9],
                                              int64_t ts, int64_t seq) {
+  const uint64_t viw = H.viw;
 #pragma unroll
   for (int x = 0; x < kMqMaxSel; ++x) {
     if (x >= nsel) break;
-    const uint64_t v = vals[Q.sel_vi[x]];
-    const int w = Q.sel_w[x];
-    if (w == 8) ((uint64_t*)Q.out_col[x])[p] = v;
-    else if (w == 4) ((uint32_t*)Q.out_col[x])[p] = (uint32_t)v;
-    else ((uint8_t*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
+    const uint32_t f = (uint32_t)(viw >> (8 * x)) & 0xffu;
+    const uint64_t v = vals[f & 15u];
+    const uint32_t w = f >> 4;
+    if (w == 8) ((uint64_t*)H.col[x])[p] = v;
+    else if (w == 4) ((uint32_t*)H.col[x])[p] = (uint32_t)v;
+    else ((uint8_t*)H.col[x])[p] = (uint8_t)(v & 1u);
   }
-  Q.out_ts[p] = ts;
-  Q.out_seq[p] = seq;
+  ((int64_t*)H.ts)[p] = ts;
+  ((int64_t*)H.seq)[p] = seq;
 }
 
 // One sequence query over a block of 64 keys (lane = key): restates
-// oracle/mq_oracle.c sequence_event for the one-partial shape.  kEmit =
-// false: returns the rows the wave would emit; true: stores them from `pos`
-// and commits the state.
+// oracle/mq_oracle.c sequence_event for the one-partial shape.  The step is
+// branch-free (selects): the kernel is issue-bound, and every divergent
+// branch costs scalar exec-mask instructions.  kEmit = false: returns the
+// rows the wave would emit; true: stores them from `pos` and commits the state.
 template <bool kEmit, int NC>
-__device__ __forceinline__ uint32_t mq_seq(const MqLds<NC>& L, const MqCtx<NC>& c, CMqQuery& Q, uint64_t* S,
-                                           int64_t ks, uint32_t maxlen, unsigned long long pos) {
+__device__ __forceinline__ uint32_t mq_seq(const MqLds<NC>& L, const MqCtx<NC>& c, CMqQuery& Q, const MqHot& H,
+                                           uint64_t* S, int64_t ks, uint32_t maxlen, unsigned long long pos) {
   // the descriptor, decoded once (uniform: scalar registers)
   const int N = Q.nstates, ncap = Q.ncap, nsel = Q.nsel;
   const uint32_t smask = Q.stream_mask, sstream = Q.st_stream, topt = Q.tail_opt;
@@ -322,84 +364,66 @@ __device__ __forceinline__ uint32_t mq_seq(const MqLds<NC>& L, const MqCtx<NC>& 
   auto stream_of = [&](int s) { return (int)((sstream >> (3 * s)) & 7u); };
   auto min_of = [&](int s) { return (uint32_t)((smin >> (8 * s)) & 0xffu); };
   auto max_of = [&](int s) { return (uint32_t)((smax >> (8 * s)) & 0xffu); };
+  const bool done0 = ((topt & 1u) != 0) && min_of(0) <= 1u;             // a start alone completes
+  const bool keep0 = N == 1 && (max_of(0) == 0xffu || 1u < max_of(0));   // ... and stays open
   for (uint32_t i = 0; i < maxlen; ++i) {
-    bool em = false;
-    int r = 0;
-    int64_t ts = 0;
-    if (i < c.len) {
-      r = L.sorted[c.r0 + i];
-      const uint64_t w0 = L.w0[r], w1 = L.w1[r];
-      const int st = mq_stream(w0);
-      if ((smask >> st) & 1u) {
-        ts = c.ts_base + (int64_t)(uint32_t)w0;
-        auto cond = [&](int s) { return ((w1 >> ((sbit >> (6 * s)) & 63u)) & 1ull) != 0; };
-        auto collect = [&](int s, bool first) {
+    const bool valid = i < c.len;
+    const int r = L.sorted[c.r0 + (valid ? i : 0u)];   // lanes past their run re-read a record
+    const uint64_t w0 = L.w0[r], w1 = L.w1[r];
+    const int st = mq_stream(w0);
+    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const bool rel = valid && ((smask >> st) & 1u) != 0;
+    auto cond = [&](int s) { return ((w1 >> ((sbit >> (6 * s)) & 63u)) & 1ull) != 0; };
+    // the live partial: expired by `within`, else stays in its count state
+    // (c1) or moves to a later state, skipping optional ones (found)
+    const int64_t d = ts - (int64_t)sts;
+    const bool alive = live && !(within >= 0 && (d < 0 ? -d : d) > within);
+    const uint32_t mj = max_of(j);
+    const bool c1 = rel && alive && stream_of(j) == st && (mj == 0xffu || cnt < mj) && cond(j);
+    bool found = false, stop = !(rel && alive && !c1 && cnt >= min_of(j));
+    int nj = j;
 #pragma unroll
-          for (int x = 0; x < kMqMaxCaps; ++x)
-            if (cst[x] == s && (clast[x] || first)) cap[x] = mq_src(L, c, csrc[x], r, ts);
-        };
-        auto settle = [&]() {
-          if (cnt >= min_of(j) && ((topt >> j) & 1u)) {
-            em = true;
-            live = j == N - 1 && (max_of(j) == 0xffu || cnt < max_of(j));
-          }
-        };
-        if (live && within >= 0) {
-          const int64_t d = ts - (int64_t)sts;
-          if ((d < 0 ? -d : d) > within) live = false;   // expired: dropped
-        }
-        if (live) {
-          bool adv = false;
-          if (stream_of(j) == st && (max_of(j) == 0xffu || cnt < max_of(j)) && cond(j)) {
-            cnt += 1;   // stay in the count state
-            collect(j, false);
-            adv = true;
-            settle();
-          } else if (cnt >= min_of(j)) {
-            bool stop = false;   // move on, skipping optional states
-            for (int j2 = 1; j2 < kMaxStates; ++j2) {
-              if (j2 >= N) break;
-              if (j2 <= j || stop) continue;
-              if (stream_of(j2) == st && cond(j2)) {
-                j = j2;
-                cnt = 1;
-                collect(j2, true);
-                adv = true;
-                stop = true;
-                settle();
-              } else if (min_of(j2) > 0) {
-                stop = true;
-              }
-            }
-          }
-          if (!adv) live = false;   // strict contiguity: discarded
-        }
-        if (stream_of(0) == st && (every || !started) && cond(0)) {
-          started = true;
-          live = true;
-          j = 0;
-          cnt = 1;
-          sts = (uint64_t)ts;
-#pragma unroll
-          for (int x = 0; x < kMqMaxCaps; ++x) cap[x] = 0;
-          collect(0, true);
-          settle();
-        }
-      }
+    for (int k = 1; k < kMaxStates; ++k) {
+      if (k >= N) break;
+      const bool inr = k > j && !stop && !found;
+      const bool hit = inr && stream_of(k) == st && cond(k);
+      nj = hit ? k : nj;
+      found = found || hit;
+      stop = stop || (inr && !hit && min_of(k) > 0u);
     }
+    const bool adv = c1 || found;
+    const int j2 = found ? nj : j;
+    const uint32_t cnt2 = found ? 1u : cnt + (c1 ? 1u : 0u);
+    const bool done2 = adv && cnt2 >= min_of(j2) && ((topt >> j2) & 1u) != 0;
+    const bool live2 = adv && (!done2 || (j2 == N - 1 && (max_of(j2) == 0xffu || cnt2 < max_of(j2))));
+    // a start event opens a new partial (never on an event that advanced one)
+    const bool start = rel && stream_of(0) == st && (every || !started) && cond(0);
+#pragma unroll
+    for (int x = 0; x < kMqMaxCaps; ++x) {
+      if (x >= ncap) break;
+      const uint64_t v = mq_src(L, c, csrc[x], r, ts);
+      const bool take = (c1 && cst[x] == j && clast[x]) || (found && cst[x] == nj);
+      cap[x] = start ? (cst[x] == 0 ? v : 0ull) : (take ? v : cap[x]);
+    }
+    const bool em = (rel && done2) || (start && done0);
+    live = start ? (!done0 || keep0) : (rel ? live2 : live);
+    j = start ? 0 : (rel ? j2 : j);
+    cnt = start ? 1u : (rel ? cnt2 : cnt);
+    sts = start ? (uint64_t)ts : sts;
+    started = started || start;
     const uint64_t m = __ballot(em);
     if (kEmit && m) {
       if (em) {
         const unsigned long long p = pos + (unsigned long long)__popcll(m & lanemask_lt());
-        if ((int64_t)p < Q.out_cap) {
-          const uint32_t row = mq_row(L.w0[r]);
+        if ((int64_t)p < H.cap) {
+          const uint32_t row = mq_row(w0);
           uint64_t vals[9];
           vals[0] = (uint64_t)c.keyv;
 #pragma unroll
           for (int y = 0; y < kMqMaxCaps; ++y) vals[1 + y] = cap[y];
 #pragma unroll
           for (int y = 5; y < 9; ++y) vals[y] = 0;
-          mq_store_row(Q, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
+          mq_store_row(H, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
         } else {
           set_err(c.err, ERR_OUT_CAP);
         }
@@ -438,109 +462,287 @@ __device__ __forceinline__ bool mq_less(uint64_t a, uint64_t b, int t) {
   }
 }
 
-// One group-by aggregation over a block of 64 keys (lane = group): running
-// values in arrival order (oracle/mq_oracle.c agg_event; sum over int / long
-// wraps in 64 bits, sum / avg over float / double accumulate in double,
-// min / max compare in the argument type), having on one output item.
+typedef __attribute__((address_space(4))) const MqUnit CMqUnit;
+
+// A class of sequence queries advanced bit-parallel (MQU_SEQ_BP): per key one
+// live mask (bit q: query q0 + q has a partial), one state, one start ts and
+// one set of captures for the whole class — every event either advances all
+// of a key's partials into the state its stream names, or (condition false,
+// move not allowed) drops them, or (the start stream) replaces them.  Same
+// semantics as mq_seq / oracle/mq_oracle.c sequence_event for this shape.
+// Per-query row counts (count pass) / output cursors (emit pass) live in the
+// wave's LDS row `cur`.
 template <bool kEmit, int NC>
-__device__ __forceinline__ uint32_t mq_agg(const MqLds<NC>& L, const MqCtx<NC>& c, CMqQuery& Q, uint64_t* S,
-                                           int64_t ks, uint32_t maxlen, unsigned long long pos) {
-  // the descriptor, decoded once (uniform: scalar registers)
-  const int in_st = Q.in_stream, fbit = Q.filter_bit, nagg = Q.nagg, nsel = Q.nsel;
-  int fn[kMqMaxAggs], at[kMqMaxAggs], asrc[kMqMaxAggs];
-  bool lsum[kMqMaxAggs];
+__device__ __forceinline__ void mq_seq_bp(const MqLds<NC>& L, const MqCtx<NC>& c, CMqUnit& U, CMqQuery* qc,
+                                          uint64_t* S, int64_t ks, uint32_t maxlen, unsigned long long* cur) {
+  CMqQuery& Q0 = qc[U.q0];
+  const int nq = U.nq, N = Q0.nstates, ncap = Q0.ncap, nsel = Q0.nsel;
+  const uint64_t qmask = nq >= 64 ? ~0ull : ((1ull << nq) - 1ull);
+  const uint32_t sos = U.st_of_stream, topt = Q0.tail_opt;
+  const uint64_t allow = U.allow, cbase = U.cbase;
+  const bool keep_last = U.keep_last != 0, every = Q0.every != 0;
+  const int64_t within = Q0.within;
+  const int lane = threadIdx.x & 63;
+  int cst[kMqMaxCaps], clast[kMqMaxCaps], csrc[kMqMaxCaps];
 #pragma unroll
-  for (int y = 0; y < kMqMaxAggs; ++y) {
-    fn[y] = y < nagg ? Q.agg_fn[y] : AGG_COUNT;
-    at[y] = Q.agg_arg_type[y];
-    asrc[y] = Q.agg_src[y];
-    lsum[y] = Q.agg_out_type[y] == T_LONG;
+  for (int x = 0; x < kMqMaxCaps; ++x) {
+    cst[x] = x < ncap ? Q0.cap_state[x] : -1;
+    clast[x] = Q0.cap_last[x];
+    csrc[x] = Q0.cap_src[x];
   }
-  const int hitem = Q.hav_item, hvi = Q.hav_vi;
-  const int htype = hitem >= 0 ? Q.sel_type[hitem] : 0;
-  const int hcop = Q.hav_cop, hctype = Q.hav_ctype;
-  const uint64_t hconst = Q.hav_cconst;
-  uint64_t cnt = 0, acc[kMqMaxAggs];
+  uint64_t live = 0, started = 0, sts = 0, cap[kMqMaxCaps];
+  int j = 0;
 #pragma unroll
-  for (int i = 0; i < kMqMaxAggs; ++i) acc[i] = 0;
+  for (int x = 0; x < kMqMaxCaps; ++x) cap[x] = 0;
   if (c.len) {
-    cnt = S[0];
+    live = S[0];
+    started = S[ks];
+    j = (int)S[2 * ks];
+    sts = S[3 * ks];
+    if (live) {
 #pragma unroll
-    for (int i = 0; i < kMqMaxAggs; ++i)
-      if (i < nagg) acc[i] = S[(int64_t)(1 + i) * ks];
+      for (int x = 0; x < kMqMaxCaps; ++x)
+        if (x < ncap) cap[x] = S[(int64_t)(4 + x) * ks];
+    }
   }
-  // the row's value slots after the current event (MqQuery::sel_vi)
-  auto fill = [&](uint64_t (&vals)[9], int r, int64_t ts) {
-    vals[0] = (uint64_t)c.keyv;
-#pragma unroll
-    for (int y = 0; y < kMqMaxAggs; ++y)
-      vals[1 + y] = fn[y] == AGG_COUNT ? cnt
-                    : fn[y] == AGG_AVG ? from_f64(as_f64(acc[y]) / (double)(int64_t)cnt)
-                                       : acc[y];
-#pragma unroll
-    for (int w = 0; w < kMqMaxCarry; ++w) vals[5 + w] = mq_src(L, c, w, r, ts);
-  };
-  uint32_t rows = 0;
   for (uint32_t i = 0; i < maxlen; ++i) {
-    bool em = false;
-    int r = 0;
-    int64_t ts = 0;
-    if (i < c.len) {
-      r = L.sorted[c.r0 + i];
-      const uint64_t w0 = L.w0[r], w1 = L.w1[r];
-      if (mq_stream(w0) == in_st && ((w1 >> fbit) & 1ull)) {
-        ts = c.ts_base + (int64_t)(uint32_t)w0;
-        const bool first = cnt == 0;
-        cnt += 1;
+    const bool valid = i < c.len;
+    const int r = L.sorted[c.r0 + (valid ? i : 0u)];   // lanes past their run re-read a record
+    const uint64_t w0 = L.w0[r], w1 = L.w1[r];
+    const int st = mq_stream(w0);
+    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const uint32_t s1 = valid ? ((sos >> (4 * st)) & 15u) : 0u;   // target state + 1 (0: not read)
+    const bool rel = s1 != 0;
+    const int s = rel ? (int)s1 - 1 : 0;
+    const int64_t d = ts - (int64_t)sts;
+    const uint64_t lv = (within >= 0 && (d < 0 ? -d : d) > within) ? 0ull : live;   // expired: dropped
+    const uint32_t cb = (uint32_t)((cbase >> (8 * s)) & 0xffu);
+    const uint64_t cm = cb == 0xffu ? qmask : ((w1 >> cb) & qmask);   // the class's conditions of state s
+    const bool isstart = rel && s == 0;
+    const uint64_t nl = isstart ? (cm & (every ? qmask : ~started))
+                                : ((((allow >> (j * 8 + s)) & 1ull) != 0) ? (lv & cm) : 0ull);
+    const bool done = ((topt >> s) & 1u) != 0;   // counts here are "at least one": satisfied on arrival
+    const uint64_t em = (rel && done) ? nl : 0ull;
+    const uint64_t after = done ? ((s == N - 1 && keep_last) ? nl : 0ull) : nl;
+    const bool first = isstart || s != j;
 #pragma unroll
-        for (int y = 0; y < kMqMaxAggs; ++y) {
-          if (fn[y] == AGG_COUNT) continue;   // (also every y >= nagg)
-          const uint64_t v = mq_src(L, c, asrc[y], r, ts);
-          if (fn[y] == AGG_SUM) {
-            acc[y] = lsum[y] ? acc[y] + v : from_f64(as_f64(acc[y]) + mq_as_double(v, at[y]));
-          } else if (fn[y] == AGG_AVG) {
-            acc[y] = from_f64(as_f64(acc[y]) + mq_as_double(v, at[y]));
-          } else if (fn[y] == AGG_MIN) {
-            if (first || mq_less(v, acc[y], at[y])) acc[y] = v;
+    for (int x = 0; x < kMqMaxCaps; ++x) {
+      if (x >= ncap) break;
+      const uint64_t v = mq_src(L, c, csrc[x], r, ts);
+      const bool take = cst[x] == s && (clast[x] || first);
+      cap[x] = !rel ? cap[x] : (take ? v : (isstart ? 0ull : cap[x]));
+    }
+    live = rel ? after : live;
+    started = isstart ? (started | nl) : started;
+    j = rel ? s : j;
+    sts = isstart ? (uint64_t)ts : sts;
+    if (__ballot(em != 0)) {   // rare: rows of this step, query by query
+      for (int q = 0; q < nq; ++q) {
+        const bool e = ((em >> q) & 1ull) != 0;
+        const uint64_t m = __ballot(e);
+        if (!m) continue;
+        if (kEmit && e) {
+          const MqHot& H = L.hot[U.q0 + q];
+          const unsigned long long p = cur[q] + (unsigned long long)__popcll(m & lanemask_lt());
+          if ((int64_t)p < H.cap) {
+            const uint32_t row = mq_row(w0);
+            uint64_t vals[9];
+            vals[0] = (uint64_t)c.keyv;
+#pragma unroll
+            for (int y = 0; y < kMqMaxCaps; ++y) vals[1 + y] = cap[y];
+#pragma unroll
+            for (int y = 5; y < 9; ++y) vals[y] = 0;
+            mq_store_row(H, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
           } else {
-            if (first || mq_less(acc[y], v, at[y])) acc[y] = v;
+            set_err(c.err, ERR_OUT_CAP);
           }
         }
-        em = true;
-        if (hitem >= 0) {
-          uint64_t vals[9];
-          fill(vals, r, ts);
-          em = vm_compare(hcop, hctype, vm_convert(vals[hvi], htype, hctype), hconst);
-        }
+        if (lane == 0) cur[q] += (unsigned long long)__popcll(m);
       }
     }
-    const uint64_t m = __ballot(em);
-    if (kEmit && m) {
-      if (em) {
-        const unsigned long long p = pos + (unsigned long long)__popcll(m & lanemask_lt());
-        if ((int64_t)p < Q.out_cap) {
-          const uint32_t row = mq_row(L.w0[r]);
-          uint64_t vals[9];
-          fill(vals, r, ts);
-          mq_store_row(Q, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
-        } else {
-          set_err(c.err, ERR_OUT_CAP);
-        }
-      }
-      pos += (unsigned long long)__popcll(m);
-    }
-    rows += (uint32_t)__popcll(m);
   }
   if (kEmit && c.len) {
-    S[0] = cnt;
+    S[0] = live;
+    S[ks] = started;
+    S[2 * ks] = (uint64_t)(uint32_t)j;
+    S[3 * ks] = sts;
+    if (live) {
 #pragma unroll
-    for (int i = 0; i < kMqMaxAggs; ++i)
-      if (i < nagg) S[(int64_t)(1 + i) * ks] = acc[i];
+      for (int x = 0; x < kMqMaxCaps; ++x)
+        if (x < ncap) S[(int64_t)(4 + x) * ks] = cap[x];
+    }
   }
-  return rows;
+}
+
+// Up to NU group-by aggregations of one shape over a block of 64 keys (lane
+// = group), each query's running values in registers (NA accumulators beside
+// the shared count): the record and the aggregate arguments are decoded once
+// per step for all of them.  Running values in arrival order as
+// oracle/mq_oracle.c agg_event (sum over int / long wraps in 64 bits, sum /
+// avg over float / double accumulate in double, min / max compare in the
+// argument type), having on one output item.  Branch-free on lane data.
+template <bool kEmit, int NC, int NU, int NA>
+__device__ __forceinline__ void mq_agg_unit(const MqLds<NC>& L, const MqCtx<NC>& c, CMqUnit& U, CMqQuery* qc,
+                                            uint64_t* state, int64_t kidx, int64_t ks, uint32_t maxlen,
+                                            unsigned long long* cur) {
+  CMqQuery& Q0 = qc[U.q0];
+  const int nq = U.nq, in_st = Q0.in_stream, nagg = Q0.nagg, nsel = Q0.nsel;
+  const int lane = threadIdx.x & 63;
+  // accumulator a <- aggregate slot; per accumulator: op (0 sum / avg in
+  // double, 1 sum in 64-bit ints, 2 min, 3 max), comparison domain (0 int64,
+  // 1 float, 2 double), argument source and type
+  int aslot[NA], aop[NA], acmp[NA], asrc[NA], atyp[NA];
+  int slot_acc[kMqMaxAggs];
+  {
+    int na = 0;
+#pragma unroll
+    for (int y = 0; y < kMqMaxAggs; ++y) {
+      slot_acc[y] = -1;
+      if (y < nagg && Q0.agg_fn[y] != AGG_COUNT && na < NA) {
+        const int fn = Q0.agg_fn[y], t = Q0.agg_arg_type[y];
+#pragma unroll
+        for (int a2 = 0; a2 < NA; ++a2)
+          if (a2 == na) {
+            aslot[a2] = y;
+            aop[a2] = fn == AGG_MIN ? 2 : fn == AGG_MAX ? 3 : (fn == AGG_SUM && Q0.agg_out_type[y] == T_LONG) ? 1 : 0;
+            acmp[a2] = (t == T_LONG || t == T_INT) ? 0 : t == T_FLOAT ? 1 : 2;
+            asrc[a2] = Q0.agg_src[y];
+            atyp[a2] = t;
+          }
+        slot_acc[y] = na++;
+      }
+    }
+#pragma unroll
+    for (int a2 = 0; a2 < NA; ++a2)
+      if (a2 >= na) { aslot[a2] = 0; aop[a2] = 0; acmp[a2] = 0; asrc[a2] = MQ_SRC_KEY; atyp[a2] = T_LONG; }
+  }
+  // having: the item's value as a double or an int64, compared with the query's constant
+  const int hitem = Q0.hav_item, hvi = Q0.hav_vi;
+  const int htype = hitem >= 0 ? Q0.sel_type[hitem] : T_LONG;
+  const int hcop = Q0.hav_cop, hctype = Q0.hav_ctype;
+  const bool hdbl = hctype == T_DOUBLE || hctype == T_FLOAT;
+  uint64_t cnt[NU], acc[NU][NA];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    cnt[i] = 0;
+#pragma unroll
+    for (int a2 = 0; a2 < NA; ++a2) acc[i][a2] = 0;
+  }
+  if (c.len) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      if (i >= nq) break;
+      const uint64_t* S = state + qc[U.q0 + i].st_off * ks + kidx;
+      cnt[i] = S[0];
+#pragma unroll
+      for (int a2 = 0; a2 < NA; ++a2)
+        if (slot_acc[aslot[a2]] == a2) acc[i][a2] = S[(int64_t)(1 + aslot[a2]) * ks];
+    }
+  }
+  // value of aggregate slot y of query i
+  auto aggval = [&](int i, int y) -> uint64_t {
+    const int fn = Q0.agg_fn[y];
+    uint64_t x = 0;
+#pragma unroll
+    for (int a2 = 0; a2 < NA; ++a2) x = slot_acc[y] == a2 ? acc[i][a2] : x;
+    return fn == AGG_COUNT ? cnt[i] : fn == AGG_AVG ? from_f64(as_f64(x) / (double)(int64_t)cnt[i]) : x;
+  };
+  for (uint32_t s = 0; s < maxlen; ++s) {
+    const bool valid = s < c.len;
+    const int r = L.sorted[c.r0 + (valid ? s : 0u)];   // lanes past their run re-read a record
+    const uint64_t w0 = L.w0[r], w1 = L.w1[r];
+    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const bool pbase = valid && mq_stream(w0) == in_st;
+    // the arguments, once for every query of the unit
+    uint64_t av[NA];
+    double ad[NA];
+#pragma unroll
+    for (int a2 = 0; a2 < NA; ++a2) {
+      av[a2] = mq_src(L, c, asrc[a2], r, ts);
+      ad[a2] = mq_as_double(av[a2], atyp[a2]);
+    }
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      if (i >= nq) break;
+      const bool pass = pbase && ((w1 >> L.hot[U.q0 + i].fbit) & 1ull) != 0;
+      const bool first = cnt[i] == 0;
+      cnt[i] += pass ? 1u : 0u;
+#pragma unroll
+      for (int a2 = 0; a2 < NA; ++a2) {
+        const uint64_t o = acc[i][a2];
+        const uint64_t sumd = from_f64(as_f64(o) + ad[a2]);
+        const uint64_t suml = o + av[a2];
+        const bool lt = acmp[a2] == 0 ? (int64_t)av[a2] < (int64_t)o
+                        : acmp[a2] == 1 ? as_f32(av[a2]) < as_f32(o) : as_f64(av[a2]) < as_f64(o);
+        const bool gt = acmp[a2] == 0 ? (int64_t)o < (int64_t)av[a2]
+                        : acmp[a2] == 1 ? as_f32(o) < as_f32(av[a2]) : as_f64(o) < as_f64(av[a2]);
+        const uint64_t nv = aop[a2] == 0 ? sumd : aop[a2] == 1 ? suml
+                            : aop[a2] == 2 ? ((first || lt) ? av[a2] : o) : ((first || gt) ? av[a2] : o);
+        acc[i][a2] = pass ? nv : o;
+      }
+      bool em = pass;
+      if (hitem >= 0) {
+        uint64_t hv = (uint64_t)c.keyv;
+        if (hvi >= 1 && hvi <= kMqMaxAggs) hv = aggval(i, hvi - 1);
+        else if (hvi >= 5) hv = mq_src(L, c, hvi - 5, r, ts);
+        const uint64_t cv = vm_convert(hv, htype, hctype);
+        bool ok;
+        if (hdbl) {
+          const double x = hctype == T_FLOAT ? (double)as_f32(cv) : as_f64(cv);
+          const uint64_t hk = L.hot[U.q0 + i].hconst;
+          const double y = hctype == T_FLOAT ? (double)as_f32(hk) : as_f64(hk);
+          ok = hcop == OP_EQ ? x == y : hcop == OP_NE ? x != y : hcop == OP_LT ? x < y
+               : hcop == OP_LE ? x <= y : hcop == OP_GT ? x > y : x >= y;
+        } else {
+          const int64_t x = hctype == T_LONG ? (int64_t)cv : (int64_t)(int32_t)cv;
+          const uint64_t hk = L.hot[U.q0 + i].hconst;
+          const int64_t y = hctype == T_LONG ? (int64_t)hk : (int64_t)(int32_t)hk;
+          ok = hcop == OP_EQ ? x == y : hcop == OP_NE ? x != y : hcop == OP_LT ? x < y
+               : hcop == OP_LE ? x <= y : hcop == OP_GT ? x > y : x >= y;
+        }
+        em = em && ok;
+      }
+      const uint64_t m = __ballot(em);
+      if (kEmit && m) {
+        if (em) {
+          const MqHot& H = L.hot[U.q0 + i];
+          const unsigned long long p = cur[i] + (unsigned long long)__popcll(m & lanemask_lt());
+          if ((int64_t)p < H.cap) {
+            const uint32_t row = mq_row(w0);
+            uint64_t vals[9];
+            vals[0] = (uint64_t)c.keyv;
+#pragma unroll
+            for (int y = 0; y < kMqMaxAggs; ++y) vals[1 + y] = y < nagg ? aggval(i, y) : 0ull;
+#pragma unroll
+            for (int w = 0; w < kMqMaxCarry; ++w) vals[5 + w] = mq_src(L, c, w, r, ts);
+            mq_store_row(H, nsel, p, vals, ts, c.in_seq ? c.in_seq[row] : c.seq_base + row);
+          } else {
+            set_err(c.err, ERR_OUT_CAP);
+          }
+        }
+      }
+      if (m && lane == 0) cur[i] += (unsigned long long)__popcll(m);
+    }
+  }
+  if (kEmit && c.len) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      if (i >= nq) break;
+      uint64_t* S = state + qc[U.q0 + i].st_off * ks + kidx;
+      S[0] = cnt[i];
+#pragma unroll
+      for (int a2 = 0; a2 < NA; ++a2)
+        if (slot_acc[aslot[a2]] == a2) S[(int64_t)(1 + aslot[a2]) * ks] = acc[i][a2];
+    }
+  }
 }
 
 }  // namespace
+
+#define MQ_STAMP(i)                                                                       \
+  do {                                                                                    \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 template <int NC>   // physical carried words per record
 __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
@@ -560,6 +762,22 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
   const int64_t ts_base = a.chunk_base[0], seq_base = a.chunk_base[1];
   CMqQuery* qc = (CMqQuery*)a.q;
   const MqCtx<NC> c0{ts_base, seq_base, 0, 0, 0, a.lmap[0], a.lmap[1], a.lmap[2], a.lmap[3], a.in_seq, a.err};
+  MQ_STAMP(0);
+  for (int q = tid; q < a.nq; q += NT) {
+    MqHot& h = L.hot[q];
+    CMqQuery& Q = qc[q];
+    uint64_t viw = 0;
+    for (int x = 0; x < kMqMaxSel; ++x) {
+      h.col[x] = x < Q.nsel ? (uint64_t)Q.out_col[x] : 0ull;
+      if (x < Q.nsel) viw |= (uint64_t)((uint32_t)Q.sel_vi[x] | ((uint32_t)Q.sel_w[x] << 4)) << (8 * x);
+    }
+    h.viw = viw;
+    h.ts = (uint64_t)Q.out_ts;
+    h.seq = (uint64_t)Q.out_seq;
+    h.cap = Q.out_cap;
+    h.hconst = Q.hav_cconst;
+    h.fbit = (uint32_t)Q.filter_bit;
+  }
   // this bucket's segment of every tile -> exclusive prefix over tiles
   {
     constexpr int MAXPER = kMqMaxTiles / NT;
@@ -651,6 +869,7 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       lds_barrier();
       nw = L.nwin;
     }
+    MQ_STAMP(1);
     if (split) {
       ++sub;
       if (sub * (uint32_t)W >= (uint32_t)kMqTile) {
@@ -719,27 +938,48 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       if (lane == 0) L.bmax[b] = len;
     }
     lds_barrier();
-    const int nitems = a.nq * nblk;
+    MQ_STAMP(2);
+    const int nitems = a.nunits * nblk;
+    CMqUnit* units = (CMqUnit*)a.units;
+    // a unit over one 64-key block (lane = key); cur: the wave's per-query
+    // row counters (count pass) / output cursors (emit pass)
+    auto run_unit = [&](auto emit, int u, int b) {
+      constexpr bool kE = decltype(emit)::value;
+      CMqUnit& U = units[u];
+      const uint32_t maxlen = L.bmax[b];
+      unsigned long long* cur = L.wcur[wave];
+      if (!maxlen) return;
+      const int k = b * 64 + lane < kpb ? L.korder[b * 64 + lane] : kpb;
+      MqCtx<NC> c = c0;
+      if (k < kpb) {
+        c.r0 = L.kstart[k];
+        c.len = L.kstart[k + 1] - c.r0;
+        c.keyv = ((((int64_t)k << lg) | bucket) * a.key_stride) + a.key_offset;
+      }
+      const int64_t kidx = (int64_t)bucket * kpb + (k < kpb ? k : 0);
+      if (U.kind == MQU_SEQ) {
+        CMqQuery& Q = qc[U.q0];
+        const unsigned long long rows = mq_seq<kE, NC>(L, c, Q, L.hot[U.q0], a.state + Q.st_off * ks + kidx, ks,
+                                                       maxlen, kE ? cur[0] : 0ull);
+        if (!kE && lane == 0) cur[0] = rows;
+      } else if (U.kind == MQU_SEQ_BP) {
+        mq_seq_bp<kE, NC>(L, c, U, qc, a.state + U.st_off * ks + kidx, ks, maxlen, cur);
+      } else if (U.nu == 8) {
+        mq_agg_unit<kE, NC, 8, 1>(L, c, U, qc, a.state, kidx, ks, maxlen, cur);
+      } else if (U.nu == 4) {
+        mq_agg_unit<kE, NC, 4, 2>(L, c, U, qc, a.state, kidx, ks, maxlen, cur);
+      } else {
+        mq_agg_unit<kE, NC, 2, 4>(L, c, U, qc, a.state, kidx, ks, maxlen, cur);
+      }
+    };
     // pass 1: rows per (query, block)
     for (int it = wave; it < nitems; it += NWV) {
-      const int q = __builtin_amdgcn_readfirstlane(it / nblk);
-      const int b = __builtin_amdgcn_readfirstlane(it - q * nblk);
-      const uint32_t maxlen = L.bmax[b];
-      uint32_t rows = 0;
-      if (maxlen) {
-        CMqQuery& Q = qc[q];
-        const int k = b * 64 + lane < kpb ? L.korder[b * 64 + lane] : kpb;
-        MqCtx<NC> c = c0;
-        if (k < kpb) {
-          c.r0 = L.kstart[k];
-          c.len = L.kstart[k + 1] - c.r0;
-          c.keyv = ((((int64_t)k << lg) | bucket) * a.key_stride) + a.key_offset;
-        }
-        uint64_t* S = a.state + Q.st_off * ks + (int64_t)bucket * kpb + (k < kpb ? k : 0);
-        rows = Q.kind == MQ_SEQ ? mq_seq<false, NC>(L, c, Q, S, ks, maxlen, 0)
-                                : mq_agg<false, NC>(L, c, Q, S, ks, maxlen, 0);
-      }
-      if (lane == 0) L.qoff[q * nblk + b] = rows;
+      const int u = __builtin_amdgcn_readfirstlane(it / nblk);
+      const int b = __builtin_amdgcn_readfirstlane(it - u * nblk);
+      const int q0 = units[u].q0, nqu = units[u].nq;
+      for (int q = lane; q < nqu; q += 64) L.wcur[wave][q] = 0;
+      run_unit(std::false_type{}, u, b);
+      for (int q = lane; q < nqu; q += 64) L.qoff[(q0 + q) * nblk + b] = (uint32_t)L.wcur[wave][q];
     }
     lds_barrier();
     // one output reservation per (window, query)
@@ -753,27 +993,18 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       L.qbase[tid] = s ? atomicAdd(qc[tid].out_count, (unsigned long long)s) : 0ull;
     }
     lds_barrier();
+    MQ_STAMP(3);
     // pass 2: rows + state commit
     for (int it = wave; it < nitems; it += NWV) {
-      const int q = __builtin_amdgcn_readfirstlane(it / nblk);
-      const int b = __builtin_amdgcn_readfirstlane(it - q * nblk);
-      const uint32_t maxlen = L.bmax[b];
-      if (!maxlen) continue;
-      CMqQuery& Q = qc[q];
-      const int k = b * 64 + lane < kpb ? L.korder[b * 64 + lane] : kpb;
-      MqCtx<NC> c = c0;
-      if (k < kpb) {
-        c.r0 = L.kstart[k];
-        c.len = L.kstart[k + 1] - c.r0;
-        c.keyv = ((((int64_t)k << lg) | bucket) * a.key_stride) + a.key_offset;
-      }
-      uint64_t* S = a.state + Q.st_off * ks + (int64_t)bucket * kpb + (k < kpb ? k : 0);
-      const unsigned long long pos = L.qbase[q] + L.qoff[q * nblk + b];
-      if (Q.kind == MQ_SEQ) mq_seq<true, NC>(L, c, Q, S, ks, maxlen, pos);
-      else mq_agg<true, NC>(L, c, Q, S, ks, maxlen, pos);
+      const int u = __builtin_amdgcn_readfirstlane(it / nblk);
+      const int b = __builtin_amdgcn_readfirstlane(it - u * nblk);
+      const int q0 = units[u].q0, nqu = units[u].nq;
+      for (int q = lane; q < nqu; q += 64) L.wcur[wave][q] = L.qbase[q0 + q] + L.qoff[(q0 + q) * nblk + b];
+      run_unit(std::true_type{}, u, b);
     }
     // the next window re-reads state this one wrote and reuses the LDS arrays
     if (t0 < ntiles) __syncthreads();
+    MQ_STAMP(4);
   }
 }
 

@@ -172,6 +172,9 @@ def rows_digest_words(key, cols, ts, seq, rank_base=None) -> int:
     k64 = key.to(torch.int64)
     rank = _key_ranks(k64)
     if rank_base is not None:
+        lo, hi = int(k64.min().item()), int(k64.max().item())
+        if lo < 0 or hi >= rank_base.shape[0]:   # (a wrong key must not index out of bounds)
+            raise ValueError("output key %d..%d outside [0, %d)" % (lo, hi, rank_base.shape[0]))
         rank = rank + rank_base[k64]
         rank_base.index_add_(0, k64, torch.ones_like(k64))
     x = _smix_t((k64 & 0xFFFFFFFF) | (rank << 32))
