@@ -78,6 +78,9 @@ def parse():
                          "ordinary host memory) instead of device-resident inputs")
     ap.add_argument("--deliver", action="store_true",
                     help="deliver every match to a host callback at each flush (pinned D2H)")
+    ap.add_argument("--ordered", action="store_true",
+                    help="with --deliver: ordered_output=1, rows sorted into Siddhi's global emission "
+                         "order on the device before the D2H (the drop-in default)")
     ap.add_argument("--parity-steps", type=int, default=4,
                     help="config 5: steps of the stream the parity check covers (fresh state)")
     return ap.parse_args()
@@ -400,6 +403,8 @@ def main():
         if args.no_parity:
             parity = None
         del w
+    if args.ordered:
+        opts["ordered_output"] = 1
     rt = fs.SiddhiAppRuntime(plan, **opts)
 
     # Inputs for every step, generated on the device before the timed region.
@@ -486,6 +491,7 @@ def main():
         for s in range(warm):
             step(batches[s])
     st0 = rt.stats()
+    d0 = delivered[0]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -620,8 +626,10 @@ def main():
             "kernels": kern,
             "parity": parity,
             "host_io": ({"ingest": args.ingest, "bytes_in_per_event": in_b,
-                         "pcie_in_GBs": round(value * in_b / 1e9, 2),
-                         "delivered_rows": delivered[0] if args.deliver else None}
+                         "pcie_in_GBs": round(value * in_b / 1e9, 2) if host_ingest else 0.0,
+                         "delivered_rows": delivered[0] - d0 if args.deliver else None,
+                         "delivered_rows_per_s": round((delivered[0] - d0) / dt_max, 1) if args.deliver else None,
+                         "ordered_output": bool(args.ordered)}
                         if host_ingest or args.deliver else None),
             "cpu_baseline": cpu,
             "speedup_vs_cpu_baseline": round(value / cpu["value"], 1) if cpu else None,

@@ -102,8 +102,10 @@ struct OutStream {
   // pinned host copies for callback delivery (D2H at PCIe speed)
   std::vector<HostBuf> hcols;
   HostBuf hts, hseq;
-  std::vector<std::vector<uint8_t>> sorted;   // ordered_output: rows permuted into emission order
-  std::vector<int64_t> sts, sseq;
+  // ordered_output: the rows permuted into Siddhi's emission order on the
+  // device (stable sort on seq) before the D2H
+  std::vector<DevBuf> scols;
+  DevBuf sts, sseq;
 };
 
 struct PatternRT {
@@ -211,7 +213,9 @@ struct cep_app {
   DevBuf rerr;                 // error word of the route kernels (route stream; the walk's is `err`)
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   DevBuf str_hash;             // Java String.hashCode per dictionary id (dynamic routing)
-  HostBuf flush_words;         // cep_flush: error word + output cursors (pinned)
+  HostBuf flush_words;         // cep_flush: error word + output cursors + seq stats (pinned)
+  DevBuf ostats;               // cep_flush: per output {~min seq, max seq, descents} (k_seq_stats)
+  DevBuf okeys[2], oidx[2], otemp;   // cep_flush: emission-order sort scratch (shared by the outputs)
   DevBuf rr_col[kMaxCols], rr_ts, rr_stream, rr_seq;   // cep_send_rows: unpacked rows
   // host batches: two staging slots (pinned host arena + device arena); a
   // batch's H2D copy runs on the copy stream while the previous batch's
@@ -1904,8 +1908,12 @@ void cep_destroy(cep_app* a) {
     for (auto& c : o.cols) dev_free(&c);
     dev_free(&o.ts);
     dev_free(&o.seq);
+    for (auto& c : o.scols) dev_free(&c);
+    dev_free(&o.sts);
+    dev_free(&o.sseq);
     if (o.count) hipFree(o.count);
   }
+  for (DevBuf* b : {&a->ostats, &a->okeys[0], &a->okeys[1], &a->oidx[0], &a->oidx[1], &a->otemp}) dev_free(b);
   for (auto& p : a->pats) {
     dev_free(&p.khdr);
     dev_free(&p.kslot);
@@ -2261,14 +2269,26 @@ int cep_watermark(cep_app* a, int64_t mark) {
 
 int cep_flush(cep_app* a) {
   if (!a) return CEP_E_ARG;
-  // the error word and every output cursor in one pinned readback, one sync
+  // the error word, every output cursor and (ordered_output) every delivered
+  // output's seq range / descents in one pinned readback, one sync
   const size_t no = a->outs.size();
-  if (!host_ensure(&a->flush_words, (no + 1) * 8)) return fail(a, CEP_E_DEVICE, "out of pinned host memory");
+  const bool order = a->opt.ordered_output != 0;
+  if (!host_ensure(&a->flush_words, (no * 4 + 1) * 8)) return fail(a, CEP_E_DEVICE, "out of pinned host memory");
   uint64_t* fw = (uint64_t*)a->flush_words.p;
+  uint64_t* fst = fw + 1 + no;   // 3 words per output
   fw[0] = 0;
+  if (order) {
+    if (!dev_ensure(&a->ostats, no * 3 * 8, a->stream, false)) return fail(a, CEP_E_DEVICE, "out of device memory");
+    hipMemsetAsync(a->ostats.p, 0, no * 3 * 8, a->stream);
+    for (size_t i = 0; i < no; ++i)
+      if (a->outs[i].fn)
+        launch_seq_stats((const int64_t*)a->outs[i].seq.p, a->outs[i].count, a->outs[i].cap,
+                         (unsigned long long*)a->ostats.p + 3 * i, a->stream);
+  }
   hipMemcpyAsync(fw, a->err.p, 4, hipMemcpyDeviceToHost, a->stream);
   for (size_t i = 0; i < no; ++i)
     hipMemcpyAsync(fw + 1 + i, a->outs[i].count, 8, hipMemcpyDeviceToHost, a->stream);
+  if (order) hipMemcpyAsync(fst, a->ostats.p, no * 3 * 8, hipMemcpyDeviceToHost, a->stream);
   if (hipStreamSynchronize(a->stream) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "device failure during processing");
   harvest_timers(a);
@@ -2287,50 +2307,62 @@ int cep_flush(cep_app* a) {
     const unsigned long long cnt = rc == CEP_OK ? fw[1 + i] : 0ull;
     a->matches_out += (int64_t)cnt;
     if (o.fn && cnt > 0 && rc == CEP_OK) {
-      // one async D2H per column into pinned buffers, one sync
       const size_t n = cnt;
+      const void* src_ts = o.ts.p;
+      const void* src_seq = o.seq.p;
+      std::vector<const void*> src(o.cols.size());
+      for (size_t c = 0; c < o.cols.size(); ++c) src[c] = o.cols[c].p;
+      if (order && fst[3 * i + 2] > 0) {
+        // Siddhi's emission order (StreamOutputHandler.java:63-92 receives
+        // each completing event's matches in turn): by completing event, then
+        // pending order, which the walk already keeps contiguous per key — a
+        // stable sort on seq over the window's seq range, then one gather
+        // per column, all on the device.
+        if (n > (size_t)INT32_MAX) return fail(a, CEP_E_DEVICE, "too many rows to order in one flush");
+        const uint64_t bias = 0x8000000000000000ull;
+        const int64_t lo = (int64_t)(~fst[3 * i] ^ bias), hi = (int64_t)(fst[3 * i + 1] ^ bias);
+        const uint64_t range = (uint64_t)hi - (uint64_t)lo;
+        const int bits = range ? 64 - __builtin_clzll(range) : 1;
+        const size_t tb = order_temp_bytes((int64_t)n);
+        bool ok = dev_ensure(&a->okeys[0], n * 8, a->stream, false) && dev_ensure(&a->okeys[1], n * 8, a->stream, false) &&
+                  dev_ensure(&a->oidx[0], n * 4, a->stream, false) && dev_ensure(&a->oidx[1], n * 4, a->stream, false) &&
+                  dev_ensure(&a->otemp, tb, a->stream, false) && dev_ensure(&o.sts, n * 8, a->stream, false) &&
+                  dev_ensure(&o.sseq, n * 8, a->stream, false);
+        o.scols.resize(o.cols.size());
+        for (size_t c = 0; c < o.cols.size() && ok; ++c)
+          ok = dev_ensure(&o.scols[c], n * type_width(o.types[c]), a->stream, false);
+        if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (output ordering)");
+        if (order_sort(a->otemp.p, a->otemp.bytes, (const int64_t*)o.seq.p, (int64_t)n, lo, bits, a->okeys[0].p,
+                       a->okeys[1].p, (int32_t*)a->oidx[0].p, (int32_t*)a->oidx[1].p, a->stream) != 0)
+          return fail(a, CEP_E_DEVICE, "output ordering sort failed");
+        const int32_t* perm = (const int32_t*)a->oidx[1].p;
+        for (size_t c = 0; c < o.cols.size(); ++c) {
+          launch_gather(o.cols[c].p, o.scols[c].p, perm, 0, (int64_t)n, type_width(o.types[c]), a->stream);
+          src[c] = o.scols[c].p;
+        }
+        launch_gather(o.ts.p, o.sts.p, perm, 0, (int64_t)n, 8, a->stream);
+        launch_gather(o.seq.p, o.sseq.p, perm, 0, (int64_t)n, 8, a->stream);
+        src_ts = o.sts.p;
+        src_seq = o.sseq.p;
+      }
+      // one async D2H per column into pinned buffers, one sync
       o.hcols.resize(o.cols.size());
       bool ok = host_ensure(&o.hts, n * 8) && host_ensure(&o.hseq, n * 8);
       for (size_t c = 0; c < o.cols.size() && ok; ++c) ok = host_ensure(&o.hcols[c], n * type_width(o.types[c]));
       if (!ok) return fail(a, CEP_E_DEVICE, "out of pinned host memory (output delivery)");
-      hipMemcpyAsync(o.hts.p, o.ts.p, n * 8, hipMemcpyDeviceToHost, a->stream);
-      hipMemcpyAsync(o.hseq.p, o.seq.p, n * 8, hipMemcpyDeviceToHost, a->stream);
+      hipMemcpyAsync(o.hts.p, src_ts, n * 8, hipMemcpyDeviceToHost, a->stream);
+      hipMemcpyAsync(o.hseq.p, src_seq, n * 8, hipMemcpyDeviceToHost, a->stream);
       for (size_t c = 0; c < o.cols.size(); ++c)
-        hipMemcpyAsync(o.hcols[c].p, o.cols[c].p, n * type_width(o.types[c]), hipMemcpyDeviceToHost, a->stream);
+        hipMemcpyAsync(o.hcols[c].p, src[c], n * type_width(o.types[c]), hipMemcpyDeviceToHost, a->stream);
       if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "output delivery failed");
-      const int64_t* hts = (const int64_t*)o.hts.p;
-      const int64_t* hseq = (const int64_t*)o.hseq.p;
       std::vector<const void*> ptrs(o.cols.size());
       for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.hcols[c].p;
-      if (a->opt.ordered_output && !std::is_sorted(hseq, hseq + n)) {
-        // Siddhi's emission order: by completing event, then by pending
-        // order (contiguous per key already) — a stable sort on seq.
-        std::vector<uint32_t> perm(n);
-        std::iota(perm.begin(), perm.end(), 0u);
-        std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) { return hseq[x] < hseq[y]; });
-        o.sorted.resize(o.cols.size());
-        for (size_t c = 0; c < o.cols.size(); ++c) {
-          const int w = type_width(o.types[c]);
-          o.sorted[c].resize(n * w);
-          const uint8_t* src = (const uint8_t*)o.hcols[c].p;
-          for (size_t i = 0; i < n; ++i) std::memcpy(&o.sorted[c][i * w], src + (size_t)perm[i] * w, w);
-          ptrs[c] = o.sorted[c].data();
-        }
-        o.sts.resize(n);
-        o.sseq.resize(n);
-        for (size_t i = 0; i < n; ++i) {
-          o.sts[i] = hts[perm[i]];
-          o.sseq[i] = hseq[perm[i]];
-        }
-        hts = o.sts.data();
-        hseq = o.sseq.data();
-      }
       cep_rows rows{};
       rows.stream_id = o.id.c_str();
       rows.n = (int64_t)n;
       rows.ncols = (int32_t)o.cols.size();
-      rows.ts = hts;
-      rows.seq = hseq;
+      rows.ts = (const int64_t*)o.hts.p;
+      rows.seq = (const int64_t*)o.hseq.p;
       rows.cols = ptrs.data();
       o.fn(o.user, &rows);
     }

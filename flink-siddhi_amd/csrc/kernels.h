@@ -549,6 +549,12 @@ int reorder_sort(void* temp, size_t temp_bytes, const int64_t* keys_in, int64_t*
 void launch_upper_bound(const int64_t* sorted, int64_t n, int64_t wm, int64_t* out3, hipStream_t s);
 void launch_gather(const void* src, void* dst, const int32_t* perm, int64_t first, int64_t n, int width,
                    hipStream_t s);
+// output emission order (reorder.hip): seq range / descents, stable seq sort
+void launch_seq_stats(const int64_t* seq, const unsigned long long* count, int64_t cap, unsigned long long* out3,
+                      hipStream_t s);
+size_t order_temp_bytes(int64_t n);
+int order_sort(void* temp, size_t temp_bytes, const int64_t* seq, int64_t n, int64_t lo, int bits, void* keys_a,
+               void* keys_b, int32_t* idx_a, int32_t* idx_b, hipStream_t s);
 void launch_generate(int64_t first, int64_t n, uint64_t seed, int64_t keys,
                      int64_t rate, int64_t t0, int single_stream, int32_t* key,
                      int64_t* ts, uint8_t* stream, int32_t* id, double* price,

@@ -117,3 +117,37 @@ def test_vm_walk_16mi_chunks_vs_oracle():
     torch.cuda.empty_cache()
     w = CO.generate(0, n, K, rate=R, threads=16)
     assert_same_per_key(got, oracle_rows(w, K))
+
+
+def test_config3_ordered_delivery_bench_geometry():
+    # ordered_output = 1 (the drop-in default): the flush sorts each output's
+    # rows by completing event on the device (stable on seq, so one event's
+    # matches keep pending order) and delivers them to the host callback in
+    # Siddhi's global emission order (StreamOutputHandler.java:63-92) — every
+    # row identical to the oracle's, in the same position.
+    import torch
+    sizes = [CHUNK + 777, 1 << 23]
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, chunk_events=CHUNK, ordered_output=1)
+    rt.add_callback("O")
+    first = 0
+    for n in sizes:
+        d = workload.generate_device(first, n, K, rate=R)
+        rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
+        rt.flush()
+        first += n
+        del d
+    out = rt.collect("O")
+    rt.shutdown()
+    torch.cuda.empty_cache()
+    w = CO.generate(0, first, K, rate=R, threads=16)
+    po = CO.PatternOracle(K, F, G, every=True, within=10000)
+    a, b, m = po.run(w)
+    order = np.lexsort((a, b))     # completing event, then pending (arrival) order
+    a, b = a[order], b[order]
+    assert m > 2_000_000 and len(out.ts) == m, (len(out.ts), m)
+    want = {"k": w["k"][a], "p1": w["price"][a], "p2": w["price"][b], "t": w["ts"][b], "ts": w["ts"][b], "seq": b}
+    got = {"k": out.cols[0], "p1": out.cols[1], "p2": out.cols[2], "t": out.cols[3], "ts": out.ts, "seq": out.seq}
+    for c in want:
+        if not np.array_equal(got[c], want[c]):
+            i = int(np.nonzero(got[c] != want[c])[0][0])
+            raise AssertionError("column %s differs at row %d: engine %r oracle %r" % (c, i, got[c][i], want[c][i]))
