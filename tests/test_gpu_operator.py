@@ -252,3 +252,53 @@ def test_operator_route_uses_each_plans_last_partition_key():
     assert "p2" not in op.route("inputStream1", cols[3], cols, 4)
     assert op.partition_keys("p2") == ["id"] and op.partition_keys("p5") == ["id", "id"]
     op.shutdown()
+
+
+def test_route_plan_over_streams_with_different_group_by_attributes():
+    # A plan reading two streams partitioned on differently named attributes:
+    # the router's key list is the concatenation of every stream's group-by
+    # list (AddRouteOperator.java:159-175), and each row takes the LAST key of
+    # that list (:83-92 overwrites setPartitionKey per key).  A stream without
+    # a field of that name sums no hashCode: partition key 0, channel 0.  An
+    # update appends the new plan's keys to the old list (:166-171).
+    schemas = {"s1": [("id", "int"), ("price", "double"), ("timestamp", "long")],
+               "s2": [("uid", "int"), ("price", "double"), ("timestamp", "long")]}
+    plan = ("partition with (id of s1, uid of s2) begin "
+            "from every a=s1[price > 0.5] -> b=s2[price < 0.3] within 1 sec "
+            "select a.id as id, b.uid as u insert into O; end;")
+    op = SiddhiOperator(schemas)
+    op.add_plan("px", plan)
+    assert op.partition_keys("px") == ["id", "uid"]
+    rng = np.random.default_rng(11)
+    n = 3000
+    ids = rng.integers(-1000, 1000, n).astype(np.int32)
+    price = rng.random(n)
+    ts = np.arange(n, dtype=np.int64)
+    cols = [torch.from_numpy(c).cuda() for c in (ids, price, ts)]
+    r1 = op.route("s1", cols[2], cols, 5, keys=True)
+    r2 = op.route("s2", cols[2], cols, 5, keys=True)
+    torch.cuda.synchronize()
+    assert (r1["px"][1].cpu().numpy() == 0).all() and (r1["px"][0].cpu().numpy() == 0).all()
+    want = np.abs(ids.astype(np.int64))
+    np.testing.assert_array_equal(r2["px"][1].cpu().numpy(), want)
+    np.testing.assert_array_equal(r2["px"][0].cpu().numpy(), want % 5)
+    # update to a plan keyed on price of s2 only: the list grows, the last key
+    # is now s1's (id): s1 rows route by id, s2 rows (no id field) to key 0
+    plan2 = ("partition with (uid of s2, id of s1) begin "
+             "from every a=s2[price > 0.5] -> b=s1[price < 0.3] within 1 sec "
+             "select a.uid as u, b.id as id insert into O; end;")
+    op.update_plan("px", plan2)
+    assert op.partition_keys("px") == ["id", "uid", "id", "uid"] or \
+        op.partition_keys("px") == ["id", "uid", "uid", "id"]
+    last = op.partition_keys("px")[-1]
+    r1 = op.route("s1", cols[2], cols, 5, keys=True)
+    r2 = op.route("s2", cols[2], cols, 5, keys=True)
+    torch.cuda.synchronize()
+    k1, k2 = r1["px"][1].cpu().numpy(), r2["px"][1].cpu().numpy()
+    if last == "id":
+        np.testing.assert_array_equal(k1, want)
+        assert (k2 == 0).all()
+    else:
+        assert (k1 == 0).all()
+        np.testing.assert_array_equal(k2, want)
+    op.shutdown()
