@@ -22,14 +22,27 @@ def _host_staged() -> bool:
     return dist.get_backend() != "nccl"
 
 
-def exchange_counts(counts: Sequence[int], device) -> List[int]:
-    """All-to-all of the per-owner record counts -> counts received from each source."""
+_COUNT_GROUP = []
+
+
+def _count_group():
+    """A gloo group beside the RCCL one for the per-owner counts: the counts
+    are host integers already (the route returns them), and RCCL's alltoallv
+    needs host split sizes, so exchanging them host to host keeps the step
+    free of a device round trip (an all-to-all of a device tensor followed by
+    a readback would wait for everything queued on torch's stream)."""
+    if not _COUNT_GROUP:
+        _COUNT_GROUP.append(dist.new_group(backend="gloo") if not _host_staged() else None)
+    return _COUNT_GROUP[0]
+
+
+def exchange_counts(counts: Sequence[int], device=None) -> List[int]:
+    """All-to-all of the per-owner record counts -> counts received from each
+    source (host to host: no GPU synchronisation)."""
     world = dist.get_world_size()
-    if _host_staged():
-        device = "cpu"
-    send = torch.tensor(list(counts), dtype=torch.int64, device=device)
-    recv = torch.empty(world, dtype=torch.int64, device=device)
-    dist.all_to_all_single(recv, send)
+    send = torch.tensor(list(counts), dtype=torch.int64)
+    recv = torch.empty(world, dtype=torch.int64)
+    dist.all_to_all_single(recv, send, group=_count_group())
     return [int(x) for x in recv.tolist()]
 
 
