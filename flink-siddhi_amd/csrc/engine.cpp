@@ -825,11 +825,30 @@ int build_mq_groups(cep_app* a) {
         const Query& q = app.queries[g.qs[q0]];
         int na = 0;
         for (auto& ag : q.aggs) na += ag.fn != AGG_COUNT ? 1 : 0;
-        const int nu = na <= 1 ? 8 : na == 2 ? 4 : 2;   // k_mqwalk's mq_agg_unit widths
+        int nu = na <= 1 ? 8 : na == 2 ? 4 : 2;   // k_mqwalk's mq_agg_unit widths
+        static const int nu_cap = std::getenv("CEP_MQ_NU") ? std::atoi(std::getenv("CEP_MQ_NU")) : 8;
+        if (nu_cap == 4 || nu_cap == 2) nu = std::min(nu, nu_cap);   // diagnostics: narrower units
+        // mq_agg_fast: at most one non-count accumulator, having compared as
+        // a double or an integer (not a float)
+        const MqQuery& d0 = g.hq[q0];
+        int fast = 0;
+        if (na <= 1 && (d0.hav_item < 0 || d0.hav_ctype == T_DOUBLE || d0.hav_ctype == T_LONG ||
+                        d0.hav_ctype == T_INT)) {
+          fast = 9;
+          for (int y = 0; y < d0.nagg; ++y) {
+            const int fn = d0.agg_fn[y], t = d0.agg_arg_type[y];
+            if (fn == AGG_COUNT) continue;
+            const int acmp = (t == T_LONG || t == T_INT) ? 0 : t == T_FLOAT ? 1 : 2;
+            (void)acmp;   // min / max: generic mq_agg_unit (fast shapes 3-8 are not built)
+            fast = (fn == AGG_MIN || fn == AGG_MAX) ? 0 : (fn == AGG_SUM && d0.agg_out_type[y] == T_LONG) ? 2 : 1;
+          }
+        }
+        static const bool no_fast = std::getenv("CEP_MQ_GENERIC") != nullptr;   // diagnostics
         for (int i = 0; i < n; i += nu) {
           u.q0 = (int)q0 + i;
           u.nq = std::min(nu, n - i);
           u.nu = nu;
+          u.fast = no_fast ? 0 : fast;
           g.units.push_back(u);
         }
       }
@@ -1630,8 +1649,14 @@ int run_mq(cep_app* a, MqRT& g, const RowsArgs& rows_all) {
   wa.key_offset = g.key_offset;
   wa.state = (uint64_t*)g.state.p;
   wa.kstride = g.kstride;
+  wa.words = g.words;
+  static const int mq_ablate = std::getenv("CEP_MQ_ABLATE") ? std::atoi(std::getenv("CEP_MQ_ABLATE")) : 0;
+  wa.ablate = mq_ablate;
   wa.err = pa.err;
-  if (a->stamps.p && (1 << g.lg) * 8 <= 2 * 4096 * 16) wa.stamps = (uint64_t*)a->stamps.p;
+  if (a->stamps.p && (1 << g.lg) * 16 <= 2 * 4096 * 16) {
+    wa.stamps = (uint64_t*)a->stamps.p;
+    hipMemsetAsync(wa.stamps, 0, (size_t)(1 << g.lg) * 16 * 8, a->stream);
+  }
   // the side stream starts after everything already queued on the main one
   hipEventRecord(a->in_ready, a->stream);
   hipStreamWaitEvent(a->side, a->in_ready, 0);
@@ -1893,14 +1918,22 @@ void cep_destroy(cep_app* a) {
   if (a->stamps.p && !a->mqs.empty()) {
     // diagnostics: mean ticks per multi-query walk phase over the last launch's buckets
     const int nb = 1 << a->mqs[0].lg;
-    std::vector<uint64_t> st((size_t)nb * 8);
+    std::vector<uint64_t> st((size_t)nb * 16);
     hipMemcpy(st.data(), a->stamps.p, st.size() * 8, hipMemcpyDeviceToHost);
-    double sum[8] = {0};
-    for (int b = 0; b < nb; ++b)
+    double sum[8] = {0}, ut[8] = {0}, p1 = 0, rs = 0;
+    for (int b = 0; b < nb; ++b) {
+      const uint64_t* x = &st[(size_t)b * 16];
       for (int i = 1; i < 5; ++i)
-        if (st[(size_t)b * 8 + i] && st[(size_t)b * 8 + i - 1]) sum[i] += (double)(st[(size_t)b * 8 + i] - st[(size_t)b * 8 + i - 1]);
-    std::fprintf(stderr, "[cep stamps] mq walk ticks/bucket: gather=%.0f sort=%.0f count=%.0f emit=%.0f\n",
-                 sum[1] / nb, sum[2] / nb, sum[3] / nb, sum[4] / nb);
+        if (x[i] && x[i - 1]) sum[i] += (double)(x[i] - x[i - 1]);
+      if (x[5] && x[2]) p1 += (double)(x[5] - x[2]);
+      if (x[3] && x[5]) rs += (double)(x[3] - x[5]);
+      for (int i = 0; i < 8; ++i) ut[i] += (double)x[8 + i];
+    }
+    std::fprintf(stderr, "[cep stamps] mq walk ticks/bucket: gather=%.0f sort=%.0f count=%.0f (pass1 %.0f, "
+                 "reserve %.0f) emit=%.0f\n", sum[1] / nb, sum[2] / nb, sum[3] / nb, p1 / nb, rs / nb, sum[4] / nb);
+    std::fprintf(stderr, "[cep stamps] mq unit ticks/bucket (units 0-3) pass1: %.0f %.0f %.0f %.0f pass2: %.0f %.0f "
+                 "%.0f %.0f\n", ut[0] / nb, ut[1] / nb, ut[2] / nb, ut[3] / nb, ut[4] / nb, ut[5] / nb,
+                 ut[6] / nb, ut[7] / nb);
   }
   harvest_timers(a);
   for (auto e : a->event_pool) hipEventDestroy(e);
@@ -2596,9 +2629,12 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
       std::vector<uint64_t> st((size_t)g.words * ks);
       hipMemcpy(st.data(), g.state.p, st.size() * 8, hipMemcpyDeviceToHost);
       std::vector<uint32_t> live;
+      // state word w of bucket-major key index i = b * kpb + k lives at
+      // (b * words + w) * kpb + k (each bucket's state is one contiguous block)
+      auto sidx = [&](int64_t i, uint32_t w) { return (size_t)(((i / kpb) * nw + w) * kpb + i % kpb); };
       for (int64_t i = 0; i < ks; ++i) {
         bool any = false;
-        for (uint32_t w = 0; w < nw && !any; ++w) any = st[(size_t)w * ks + i] != 0;
+        for (uint32_t w = 0; w < nw && !any; ++w) any = st[sidx(i, w)] != 0;
         if (any) live.push_back((uint32_t)i);
       }
       const uint32_t nl = (uint32_t)live.size();
@@ -2608,7 +2644,7 @@ int cep_snapshot(cep_app* a, uint8_t** buf, size_t* len) {
       for (uint32_t i : live) {
         const uint32_t key = (uint32_t)(((i % kpb) << g.lg) | (i / kpb));   // dense key
         put(&key, 4);
-        for (uint32_t w = 0; w < nw; ++w) put(&st[(size_t)w * ks + i], 8);
+        for (uint32_t w = 0; w < nw; ++w) put(&st[sidx(i, w)], 8);
       }
     }
   }
@@ -2769,7 +2805,8 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
         get(&key, 4);
         if (key >= kc) return fail(a, CEP_E_STATE, "corrupt snapshot");
         const int64_t idx = (int64_t)(key & ((1u << g.lg) - 1)) * g.kpb + (key >> g.lg);
-        for (uint32_t w = 0; w < nw; ++w) get(&mst[gi][(size_t)w * g.kstride + idx], 8);
+        for (uint32_t w = 0; w < nw; ++w)
+          get(&mst[gi][(size_t)(((idx / g.kpb) * nw + w) * g.kpb + idx % g.kpb)], 8);
       }
     }
   } else if (!a->mqs.empty()) {

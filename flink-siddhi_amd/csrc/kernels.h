@@ -472,6 +472,8 @@ struct MqUnit {
   int32_t kind;
   int32_t q0, nq;                 // descriptors [q0, q0 + nq)
   int32_t nu;                     // MQU_AGG: queries held in registers (template width)
+  int32_t fast;                   // MQU_AGG: mq_agg_fast shape (0: generic mq_agg_unit; 1 sum / avg double,
+                                  // 2 sum long, 9 count only)
   // MQU_SEQ_BP: class state words at st_off (live mask, started mask, state, start ts, captures)
   int64_t st_off;
   uint32_t st_of_stream;          // 4 bits per input handle: state + 1 (0: the class does not read it)
@@ -516,9 +518,12 @@ struct MqWalkArgs {
   int32_t key_stride, key_offset;
   const int64_t* chunk_base;
   const int64_t* in_seq;          // per-row arrival numbers of the chunk (row shuffle), or nullptr
-  uint64_t* state;                // per-query SoA state words over the bucket-major key index
+  uint64_t* state;                // per bucket, per state word, the bucket's kpb keys: bucket b's state
+                                  // is one contiguous block of words * kpb (few pages per workgroup)
   int64_t kstride;
-  uint64_t* stamps;               // diagnostics (CEP_STAMPS=1): per bucket 8 s_memtime stamps
+  int64_t words;                  // state words per key
+  uint64_t* stamps;               // diagnostics (CEP_STAMPS=1): per bucket 16 s_memtime stamps
+  int32_t ablate;                 // diagnostics (CEP_MQ_ABLATE): 1 = rows counted, not stored
   unsigned int* err;
 };
 

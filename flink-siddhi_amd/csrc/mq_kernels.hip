@@ -260,8 +260,6 @@ struct MqLds {
   uint32_t bmax[kMqMaxKpb / 64];         // longest key run per 64-key block
   uint16_t korder[kMqMaxKpb];            // keys by descending run length (lane blocks of alike runs)
   uint32_t lhist[257];                   // run-length bins (descending), then their cursors
-  uint32_t qoff[kMqMaxQ * (kMqMaxKpb / 64)];   // per (query, block): rows, then first row
-  unsigned long long qbase[kMqMaxQ];
   unsigned long long wcur[kMqWalkThreads / 64][kMqMaxQ];   // per wave: a unit's row counts / output cursors
   MqHot hot[kMqMaxQ];                    // per query: what the step loops read (outputs, filter, having constant)
   uint32_t seg[kMqMaxTiles + 1];         // exclusive prefix of the bucket's tile segments
@@ -285,6 +283,7 @@ struct MqCtx {
   int32_t lmap0, lmap1, lmap2, lmap3;   // logical carried word -> physical (-1: event ts)
   const int64_t* in_seq;
   unsigned int* err;
+  int ablate;
 };
 
 // Logical carried word `src` (uniform) of window record r (MQ_SRC_*: key /
@@ -309,6 +308,13 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // register read and one store per column, unrolled.
 __device__ __forceinline__ void mq_store_row(const MqHot& H, int nsel, unsigned long long p, const uint64_t (&vals)[9],
                                              int64_t ts, int64_t seq) {
+  // The column pointers come from LDS, so the compiler cannot infer their
+  // address space: generic (flat) stores would count against lgkmcnt too, and
+  // every later LDS read of the step loop would wait for them to reach
+  // memory.  They are global buffers: store through global pointers.
+  typedef __attribute__((address_space(1))) uint64_t g64;
+  typedef __attribute__((address_space(1))) uint32_t g32;
+  typedef __attribute__((address_space(1))) uint8_t g8;
   const uint64_t viw = H.viw;
 #pragma unroll
   for (int x = 0; x < kMqMaxSel; ++x) {
@@ -316,12 +322,12 @@ __device__ __forceinline__ void mq_store_row(const MqHot& H, int nsel, unsigned 
     const uint32_t f = (uint32_t)(viw >> (8 * x)) & 0xffu;
     const uint64_t v = vals[f & 15u];
     const uint32_t w = f >> 4;
-    if (w == 8) ((uint64_t*)H.col[x])[p] = v;
-    else if (w == 4) ((uint32_t*)H.col[x])[p] = (uint32_t)v;
-    else ((uint8_t*)H.col[x])[p] = (uint8_t)(v & 1u);
+    if (w == 8) ((g64*)(uintptr_t)H.col[x])[p] = v;
+    else if (w == 4) ((g32*)(uintptr_t)H.col[x])[p] = (uint32_t)v;
+    else ((g8*)(uintptr_t)H.col[x])[p] = (uint8_t)(v & 1u);
   }
-  ((int64_t*)H.ts)[p] = ts;
-  ((int64_t*)H.seq)[p] = seq;
+  ((g64*)(uintptr_t)H.ts)[p] = (uint64_t)ts;
+  ((g64*)(uintptr_t)H.seq)[p] = (uint64_t)seq;
 }
 
 // One sequence query over a block of 64 keys (lane = key): restates
@@ -737,11 +743,193 @@ __device__ __forceinline__ void mq_agg_unit(const MqLds<NC>& L, const MqCtx<NC>&
   }
 }
 
+
+// Bit-pattern select without a branch (the compiler turns ternaries on
+// wave-uniform values into scalar branches, each followed by waits).
+__device__ __forceinline__ uint64_t msel(bool c, uint64_t a, uint64_t b) {
+  const uint64_t m = 0ull - (uint64_t)c;
+  return (a & m) | (b & ~m);
+}
+
+// A vmcnt(0) wait (gfx9 s_waitcnt encoding: expcnt / lgkmcnt left at max).
+// Issued after a unit's state loads so the step loop starts with no loads in
+// flight: the waitcnt pass then keeps vmcnt waits out of the loop, where they
+// would also wait for every output store issued by earlier steps (on CDNA
+// vmcnt counts stores too).
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0f70); }
+
+// Up to NU group-by aggregations of one shape with at most one non-count
+// accumulator, its operation fixed at compile time (AOP 0: sum / avg in
+// double, 1: sum in 64-bit ints, 2: min, 3: max, 4: count only; ACMP: min /
+// max domain 0 int64, 1 float, 2 double).  Same running values, having and
+// rows as mq_agg_unit (oracle/mq_oracle.c agg_event), with the per-step code
+// free of branches on descriptor values: those are decoded once per item.
+template <bool kEmit, int NC, int NU, int AOP, int ACMP>
+__device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>& c, CMqUnit& U, CMqQuery* qc,
+                                            uint64_t* state, int64_t kidx, int64_t ks, uint32_t maxlen,
+                                            unsigned long long* cur) {
+  CMqQuery& Q0 = qc[U.q0];
+  const int nq = U.nq, in_st = Q0.in_stream, nagg = Q0.nagg, nsel = Q0.nsel;
+  const int lane = threadIdx.x & 63;
+  int ys = -1;   // the accumulator's aggregate slot
+#pragma unroll
+  for (int y = 0; y < kMqMaxAggs; ++y)
+    if (y < nagg && Q0.agg_fn[y] != AGG_COUNT) ys = y;
+  const int asrc = ys >= 0 ? Q0.agg_src[ys] : (int)MQ_SRC_KEY;
+  const int atyp = ys >= 0 ? Q0.agg_arg_type[ys] : (int)T_LONG;
+  // value kinds (having item, select items): 0 key, 1 count, 2 accumulator,
+  // 3 average, 4 + w carried word w
+  auto vkind = [&](int vi) {
+    if (vi >= 5) return 4 + (vi - 5);
+    if (vi >= 1) {
+      const int fn = Q0.agg_fn[vi - 1];
+      return fn == AGG_COUNT ? 1 : fn == AGG_AVG ? 3 : 2;
+    }
+    return 0;
+  };
+  const bool hav = Q0.hav_item >= 0;
+  const int hk = hav ? vkind(Q0.hav_vi) : 0;
+  const int htype = hav ? Q0.sel_type[Q0.hav_item] : (int)T_LONG;
+  const bool hdbl = Q0.hav_ctype == T_DOUBLE;
+  const int hcop = Q0.hav_cop;
+  const bool mlt = hcop == OP_LT || hcop == OP_LE || hcop == OP_NE;
+  const bool meq = hcop == OP_EQ || hcop == OP_LE || hcop == OP_GE;
+  const bool mgt = hcop == OP_GT || hcop == OP_GE || hcop == OP_NE;
+  const bool mne = hcop == OP_NE;
+  uint32_t fbit[NU];
+  uint64_t hconst[NU], cnt[NU], acc[NU];
+  unsigned long long curv[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    fbit[i] = i < nq ? L.hot[U.q0 + i].fbit : 0u;
+    hconst[i] = i < nq ? L.hot[U.q0 + i].hconst : 0ull;
+    curv[i] = i < nq ? cur[i] : 0ull;
+    cnt[i] = 0;
+    acc[i] = 0;
+  }
+  if (c.len) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      if (i >= nq) break;
+      const uint64_t* S = state + qc[U.q0 + i].st_off * ks + kidx;
+      cnt[i] = S[0];
+      if (AOP != 4) acc[i] = S[(int64_t)(1 + ys) * ks];
+    }
+  }
+  wait_vm();
+  // the unit's select layout (one shape per unit): value kind and width per
+  // column, decoded once (wave-uniform, scalar registers)
+  int ckind[kMqMaxSel], cw[kMqMaxSel];
+#pragma unroll
+  for (int x = 0; x < kMqMaxSel; ++x) {
+    ckind[x] = x < nsel ? vkind(Q0.sel_vi[x]) : 0;
+    cw[x] = x < nsel ? Q0.sel_w[x] : 8;
+  }
+  auto todouble = [](uint64_t v, int t) {
+    const double di = (double)(int32_t)v, dl = (double)(int64_t)v, df = (double)as_f32(v);
+    return t == T_INT ? di : t == T_LONG ? dl : t == T_FLOAT ? df : as_f64(v);
+  };
+  for (uint32_t st = 0; st < maxlen; ++st) {
+    const bool valid = st < c.len;
+    const int r = L.sorted[c.r0 + (valid ? st : 0u)];   // lanes past their run re-read a record
+    const uint64_t w0 = L.w0[r], w1 = L.w1[r];
+    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const bool pbase = valid && mq_stream(w0) == in_st;
+    const uint64_t av = AOP == 4 ? 0ull : mq_src(L, c, asrc, r, ts);
+    const double ad = AOP == 0 ? todouble(av, atyp) : 0.0;
+    const uint64_t hcar = hk >= 4 ? mq_src(L, c, hk - 4, r, ts) : 0ull;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      if (i >= nq) break;
+      const bool pass = pbase && ((w1 >> fbit[i]) & 1ull) != 0;
+      const uint64_t o = acc[i];
+      const bool first = cnt[i] == 0;
+      cnt[i] += pass ? 1u : 0u;
+      uint64_t nv = o;
+      if (AOP == 0) nv = from_f64(as_f64(o) + ad);
+      if (AOP == 1) nv = o + av;
+      if (AOP == 2 || AOP == 3) {
+        const bool lt = ACMP == 0 ? (int64_t)av < (int64_t)o : ACMP == 1 ? as_f32(av) < as_f32(o)
+                                                                         : as_f64(av) < as_f64(o);
+        const bool gt = ACMP == 0 ? (int64_t)o < (int64_t)av : ACMP == 1 ? as_f32(o) < as_f32(av)
+                                                                         : as_f64(o) < as_f64(av);
+        nv = (first || (AOP == 2 ? lt : gt)) ? av : o;
+      }
+      if (AOP != 4) acc[i] = pass ? nv : o;
+      const uint64_t avgb = AOP == 0 ? from_f64(as_f64(acc[i]) / (double)(int64_t)cnt[i]) : 0ull;
+      bool em = pass;
+      if (hav) {
+        const uint64_t hv = msel(hk == 0, (uint64_t)c.keyv,
+                                 msel(hk == 1, cnt[i], msel(hk == 2, acc[i], msel(hk == 3, avgb, hcar))));
+        bool lt, eq, gt;
+        if (hdbl) {
+          const double x = todouble(hv, htype), y = as_f64(hconst[i]);
+          lt = x < y; eq = x == y; gt = x > y;
+        } else {
+          const int64_t x = Q0.hav_ctype == T_LONG ? (int64_t)hv : (int64_t)(int32_t)hv;
+          const int64_t y = Q0.hav_ctype == T_LONG ? (int64_t)hconst[i] : (int64_t)(int32_t)hconst[i];
+          lt = x < y; eq = x == y; gt = x > y;
+        }
+        em = em && (mne ? !eq : ((lt && mlt) || (eq && meq) || (gt && mgt)));
+      }
+      const uint64_t m = __ballot(em);
+      if (kEmit && m) {
+        // the row: output pointers through the constant address space (scalar
+        // loads, no LDS round trip per column), values by the decoded kinds
+        CMqQuery& Q = qc[U.q0 + i];
+        typedef __attribute__((address_space(1))) uint64_t g64;
+        typedef __attribute__((address_space(1))) uint32_t g32;
+        typedef __attribute__((address_space(1))) uint8_t g8;
+        const unsigned long long p = curv[i] + (unsigned long long)__popcll(m & lanemask_lt());
+        if (em && (int64_t)p < Q.out_cap && !(c.ablate & 1)) {
+          const uint32_t row = mq_row(w0);
+#pragma unroll
+          for (int x = 0; x < kMqMaxSel; ++x) {
+            if (x >= nsel) break;
+            const int k = ckind[x];
+            const uint64_t v = k == 0 ? (uint64_t)c.keyv : k == 1 ? cnt[i] : k == 2 ? acc[i] : k == 3 ? avgb
+                               : mq_src(L, c, k - 4, r, ts);
+            if (cw[x] == 8) ((g64*)Q.out_col[x])[p] = v;
+            else if (cw[x] == 4) ((g32*)Q.out_col[x])[p] = (uint32_t)v;
+            else ((g8*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
+          }
+          ((g64*)Q.out_ts)[p] = (uint64_t)ts;
+          ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
+        } else if (em && (int64_t)p >= Q.out_cap) {
+          set_err(c.err, ERR_OUT_CAP);
+        }
+      }
+      curv[i] += (unsigned long long)__popcll(m);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i)
+      if (i < nq) cur[i] = curv[i];
+  }
+  if (kEmit && c.len) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      if (i >= nq) break;
+      uint64_t* S = state + qc[U.q0 + i].st_off * ks + kidx;
+      S[0] = cnt[i];
+      if (AOP != 4) S[(int64_t)(1 + ys) * ks] = acc[i];
+    }
+  }
+}
+
 }  // namespace
 
 #define MQ_STAMP(i)                                                                       \
   do {                                                                                    \
-    if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (a.stamps && threadIdx.x == 0) a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// diagnostics: ticks of unit u (< 4) summed over its items, pass p, slot 8 + 4 p + u
+#define MQ_UNIT_TICKS(p, u, t0)                                                            \
+  do {                                                                                    \
+    if (a.stamps && (threadIdx.x & 63) == 0 && (u) < 4)                                   \
+      atomicAdd((unsigned long long*)&a.stamps[(int64_t)blockIdx.x * 16 + 8 + 4 * (p) + (u)], \
+                (unsigned long long)(__builtin_amdgcn_s_memtime() - (t0)));                \
   } while (0)
 
 template <int NC>   // physical carried words per record
@@ -758,10 +946,12 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
   const int nblk = (kpb + 63) >> 6;
   const int ntiles = a.ntiles;
   const int RW = 2 + NC;
-  const int64_t ks = a.kstride;
+  // this bucket's state block: word w of key k at state_b[w * kpb + k]
+  const int64_t ks = kpb;
+  uint64_t* const state_b = a.state + (int64_t)bucket * a.words * kpb;
   const int64_t ts_base = a.chunk_base[0], seq_base = a.chunk_base[1];
   CMqQuery* qc = (CMqQuery*)a.q;
-  const MqCtx<NC> c0{ts_base, seq_base, 0, 0, 0, a.lmap[0], a.lmap[1], a.lmap[2], a.lmap[3], a.in_seq, a.err};
+  const MqCtx<NC> c0{ts_base, seq_base, 0, 0, 0, a.lmap[0], a.lmap[1], a.lmap[2], a.lmap[3], a.in_seq, a.err, a.ablate};
   MQ_STAMP(0);
   for (int q = tid; q < a.nq; q += NT) {
     MqHot& h = L.hot[q];
@@ -956,52 +1146,57 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
         c.len = L.kstart[k + 1] - c.r0;
         c.keyv = ((((int64_t)k << lg) | bucket) * a.key_stride) + a.key_offset;
       }
-      const int64_t kidx = (int64_t)bucket * kpb + (k < kpb ? k : 0);
+      const int64_t kidx = k < kpb ? k : 0;
       if (U.kind == MQU_SEQ) {
         CMqQuery& Q = qc[U.q0];
-        const unsigned long long rows = mq_seq<kE, NC>(L, c, Q, L.hot[U.q0], a.state + Q.st_off * ks + kidx, ks,
+        const unsigned long long rows = mq_seq<kE, NC>(L, c, Q, L.hot[U.q0], state_b + Q.st_off * ks + kidx, ks,
                                                        maxlen, kE ? cur[0] : 0ull);
         if (!kE && lane == 0) cur[0] = rows;
       } else if (U.kind == MQU_SEQ_BP) {
-        mq_seq_bp<kE, NC>(L, c, U, qc, a.state + U.st_off * ks + kidx, ks, maxlen, cur);
+        mq_seq_bp<kE, NC>(L, c, U, qc, state_b + U.st_off * ks + kidx, ks, maxlen, cur);
+      } else if (U.fast) {
+        // the shapes built in (the rest run mq_agg_unit): compile time and
+        // code size grow with every instance
+        switch (U.fast) {
+          case 1: mq_agg_fast<kE, NC, 8, 0, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
+          case 2: mq_agg_fast<kE, NC, 8, 1, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
+          default: mq_agg_fast<kE, NC, 8, 4, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
+        }
       } else if (U.nu == 8) {
-        mq_agg_unit<kE, NC, 8, 1>(L, c, U, qc, a.state, kidx, ks, maxlen, cur);
+        mq_agg_unit<kE, NC, 8, 1>(L, c, U, qc, state_b, kidx, ks, maxlen, cur);
       } else if (U.nu == 4) {
-        mq_agg_unit<kE, NC, 4, 2>(L, c, U, qc, a.state, kidx, ks, maxlen, cur);
+        mq_agg_unit<kE, NC, 4, 2>(L, c, U, qc, state_b, kidx, ks, maxlen, cur);
       } else {
-        mq_agg_unit<kE, NC, 2, 4>(L, c, U, qc, a.state, kidx, ks, maxlen, cur);
+        mq_agg_unit<kE, NC, 2, 4>(L, c, U, qc, state_b, kidx, ks, maxlen, cur);
       }
     };
-    // pass 1: rows per (query, block)
+    // Each item (unit x 64-key block) is complete inside its wave: a count
+    // pass, one output reservation per query of the unit with rows (lane q
+    // reserves for query q0 + q), the emit pass with the state commit.  No
+    // workgroup barrier between the passes: waves run their items
+    // independently, and a key's rows of one query come from one item, so
+    // they stay in arrival order.  The emit pass re-reads the state the count
+    // pass just read (L1 / L2).
     for (int it = wave; it < nitems; it += NWV) {
       const int u = __builtin_amdgcn_readfirstlane(it / nblk);
       const int b = __builtin_amdgcn_readfirstlane(it - u * nblk);
       const int q0 = units[u].q0, nqu = units[u].nq;
       for (int q = lane; q < nqu; q += 64) L.wcur[wave][q] = 0;
+      __threadfence_block();
+      const uint64_t tu = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
       run_unit(std::false_type{}, u, b);
-      for (int q = lane; q < nqu; q += 64) L.qoff[(q0 + q) * nblk + b] = (uint32_t)L.wcur[wave][q];
-    }
-    lds_barrier();
-    // one output reservation per (window, query)
-    if (tid < a.nq) {
-      uint32_t s = 0;
-      for (int b = 0; b < nblk; ++b) {
-        const uint32_t c = L.qoff[tid * nblk + b];
-        L.qoff[tid * nblk + b] = s;
-        s += c;
+      MQ_UNIT_TICKS(0, u, tu);
+      __threadfence_block();
+      for (int q = lane; q < nqu; q += 64) {
+        const unsigned long long n = L.wcur[wave][q];
+        L.wcur[wave][q] = n ? atomicAdd(qc[q0 + q].out_count, n) : 0ull;
       }
-      L.qbase[tid] = s ? atomicAdd(qc[tid].out_count, (unsigned long long)s) : 0ull;
-    }
-    lds_barrier();
-    MQ_STAMP(3);
-    // pass 2: rows + state commit
-    for (int it = wave; it < nitems; it += NWV) {
-      const int u = __builtin_amdgcn_readfirstlane(it / nblk);
-      const int b = __builtin_amdgcn_readfirstlane(it - u * nblk);
-      const int q0 = units[u].q0, nqu = units[u].nq;
-      for (int q = lane; q < nqu; q += 64) L.wcur[wave][q] = L.qbase[q0 + q] + L.qoff[(q0 + q) * nblk + b];
+      __threadfence_block();
+      const uint64_t tv = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
       run_unit(std::true_type{}, u, b);
+      MQ_UNIT_TICKS(1, u, tv);
     }
+    MQ_STAMP(3);
     // the next window re-reads state this one wrote and reuses the LDS arrays
     if (t0 < ntiles) __syncthreads();
     MQ_STAMP(4);
