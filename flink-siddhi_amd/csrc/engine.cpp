@@ -683,7 +683,7 @@ int build_mq_groups(cep_app* a) {
     chunk = std::min<int64_t>(chunk, (int64_t)kMqMaxTiles * kMqTile);
     g.chunk = (chunk / kMqTile) * kMqTile;
     const int nphys_max = std::min<int>((int)g.carry.size(), kMqMaxPhys);
-    const int W = nphys_max <= 1 ? kMqWindow : (nphys_max == 2 ? 3072 : 2048);
+    const int W = mq_window(nphys_max);
     // keys per bucket: about half a window of records per bucket per chunk
     int64_t kpb = 64;
     while (kpb * 2 <= kMqMaxKpb && (double)g.chunk * (double)(kpb * 2) / (double)K <= W / 2) kpb *= 2;
@@ -844,6 +844,7 @@ int build_mq_groups(cep_app* a) {
           }
         }
         static const bool no_fast = std::getenv("CEP_MQ_GENERIC") != nullptr;   // diagnostics
+        if (fast && !no_fast) nu = std::min(nu, 4);   // mq_agg_fast is built 4 queries wide
         for (int i = 0; i < n; i += nu) {
           u.q0 = (int)q0 + i;
           u.nq = std::min(nu, n - i);

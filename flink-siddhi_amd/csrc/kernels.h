@@ -414,6 +414,10 @@ constexpr int kMqWindow = 4096;        // records per walk window (LDS)
 constexpr int kMqMaxTiles = (16 << 20) / kMqTile;   // chunk <= 16 Mi rows
 constexpr int kMqMaxKpb = 1024;        // keys per bucket
 constexpr int kMqMaxBuckets = 8192;
+// Records per k_mqwalk LDS window by physical carried words: what fits beside
+// the per-wave row staging (kMqStgWords) under 160 KB of LDS.
+constexpr int mq_window(int nc) { return nc <= 0 ? 4096 : nc == 1 ? 3072 : nc <= 3 ? 2048 : 1536; }
+constexpr int kMqStgWords = 320;       // per wave: staged output rows (column-major)
 enum : int32_t { MQ_SEQ = 0, MQ_AGG = 1 };
 enum : int32_t { MQ_SRC_KEY = 14, MQ_SRC_TS = 15 };   // capture / carried sources beside words 0..3
 

@@ -235,7 +235,6 @@ void launch_mq_partition(const MqPartArgs& a, hipStream_t s) {
 // ============================================================== k_mqwalk ==
 namespace {
 
-constexpr int mq_window(int nc) { return nc <= 1 ? kMqWindow : (nc == 2 ? 3072 : 2048); }
 
 // Per-query data the step loops read, staged in LDS at kernel start: read
 // where used (a scalar copy of every query's output pointers would not fit
@@ -262,6 +261,7 @@ struct MqLds {
   uint32_t lhist[257];                   // run-length bins (descending), then their cursors
   unsigned long long wcur[kMqWalkThreads / 64][kMqMaxQ];   // per wave: a unit's row counts / output cursors
   MqHot hot[kMqMaxQ];                    // per query: what the step loops read (outputs, filter, having constant)
+  uint64_t stg[kMqWalkThreads / 64][kMqStgWords];   // per wave: output rows staged for full-width stores
   uint32_t seg[kMqMaxTiles + 1];         // exclusive prefix of the bucket's tile segments
   uint16_t lo[kMqMaxTiles];              // segment start inside each tile
   uint32_t scratch[kMqWalkThreads / 64 + 1];
@@ -758,6 +758,15 @@ __device__ __forceinline__ uint64_t msel(bool c, uint64_t a, uint64_t b) {
 // vmcnt counts stores too).
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0f70); }
 
+// LDS written by some lanes of a wave, then read by others: the wave's LDS
+// operations complete in order, so a compiler fence plus an lgkmcnt(0) wait
+// is enough.  (__threadfence_block would also wait for every global store in
+// flight: on CDNA vmcnt counts stores.)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+}
+
 // Up to NU group-by aggregations of one shape with at most one non-count
 // accumulator, its operation fixed at compile time (AOP 0: sum / avg in
 // double, 1: sum in 64-bit ints, 2: min, 3: max, 4: count only; ACMP: min /
@@ -796,13 +805,12 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
   const bool meq = hcop == OP_EQ || hcop == OP_LE || hcop == OP_GE;
   const bool mgt = hcop == OP_GT || hcop == OP_GE || hcop == OP_NE;
   const bool mne = hcop == OP_NE;
-  uint32_t fbit[NU];
-  uint64_t hconst[NU], cnt[NU], acc[NU];
+  // per query: filter bit and having constant through the constant address
+  // space (scalar loads where used), running values and cursor in registers
+  uint64_t cnt[NU], acc[NU];
   unsigned long long curv[NU];
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
-    fbit[i] = i < nq ? L.hot[U.q0 + i].fbit : 0u;
-    hconst[i] = i < nq ? L.hot[U.q0 + i].hconst : 0ull;
     curv[i] = i < nq ? cur[i] : 0ull;
     cnt[i] = 0;
     acc[i] = 0;
@@ -829,19 +837,84 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
     const double di = (double)(int32_t)v, dl = (double)(int64_t)v, df = (double)as_f32(v);
     return t == T_INT ? di : t == T_LONG ? dl : t == T_FLOAT ? df : as_f64(v);
   };
+  const bool need_avg = hk == 3 || [&] {
+    bool any = false;
+#pragma unroll
+    for (int x = 0; x < kMqMaxSel; ++x) any = any || (x < nsel && ckind[x] == 3);
+    return any;
+  }();
+  // Emit pass: one query at a time, its rows staged in the wave's LDS rows
+  // (column-major, `scap` rows) and written as contiguous runs of up to scap
+  // rows per column: a step emits ~10 rows of a query, so per-step stores
+  // would write short runs of many open lines.
+  const int ncols = nsel + 2;
+  const uint32_t scap = (uint32_t)(kMqStgWords / ncols);
+  uint64_t* stg = const_cast<uint64_t*>(L.stg[threadIdx.x >> 6]);
+  const int nq_outer = kEmit ? nq : 1;
+  for (int qi = 0; qi < nq_outer; ++qi) {
+  uint32_t sc = 0;                                       // staged rows
+  unsigned long long opos = kEmit ? curv[qi] : 0ull;    // output row of the first staged row
+  auto flush = [&](CMqQuery& Q) {
+    typedef __attribute__((address_space(1))) uint64_t g64;
+    typedef __attribute__((address_space(1))) uint32_t g32;
+    typedef __attribute__((address_space(1))) uint8_t g8;
+    wave_lds_sync();
+    for (uint32_t j = lane; j < sc; j += 64) {
+      const unsigned long long p = opos + j;
+      if ((int64_t)p >= Q.out_cap) {
+        set_err(c.err, ERR_OUT_CAP);
+        continue;
+      }
+      if (c.ablate & 1) continue;
+#pragma unroll
+      for (int x = 0; x < kMqMaxSel; ++x) {
+        if (x >= nsel) break;
+        const uint64_t v = stg[x * scap + j];
+        if (cw[x] == 8) ((g64*)Q.out_col[x])[p] = v;
+        else if (cw[x] == 4) ((g32*)Q.out_col[x])[p] = (uint32_t)v;
+        else ((g8*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
+      }
+      ((g64*)Q.out_ts)[p] = stg[nsel * scap + j];
+      ((g64*)Q.out_seq)[p] = stg[(nsel + 1) * scap + j];
+    }
+    wave_lds_sync();
+    opos += sc;
+    sc = 0;
+  };
+  // The step loop is a chain of LDS reads (run slot -> record -> argument)
+  // with few waves per SIMD to hide it: the next step's record is read one
+  // step ahead and the slot after it two steps ahead.
+  const int aw = (AOP == 4 || asrc == MQ_SRC_KEY || asrc == MQ_SRC_TS) ? -1
+                 : (asrc == 0 ? c.lmap0 : asrc == 1 ? c.lmap1 : asrc == 2 ? c.lmap2 : c.lmap3);
+  auto slot_of = [&](uint32_t st) { return (int)L.sorted[c.r0 + (st < c.len ? st : 0u)]; };
+  auto car_of = [&](int r) -> uint64_t {
+    if constexpr (NC > 0) return aw >= 0 ? L.car[r * NC + (NC > 1 ? aw : 0)] : 0ull;
+    return 0ull;
+  };
+  int rn = slot_of(0);
+  uint64_t nw0 = L.w0[rn], nw1 = L.w1[rn], ncar = car_of(rn);
+  int rnn = slot_of(1);
   for (uint32_t st = 0; st < maxlen; ++st) {
     const bool valid = st < c.len;
-    const int r = L.sorted[c.r0 + (valid ? st : 0u)];   // lanes past their run re-read a record
-    const uint64_t w0 = L.w0[r], w1 = L.w1[r];
+    const int r = rn;   // lanes past their run re-read a record
+    const uint64_t w0 = nw0, w1 = nw1, car = ncar;
+    rn = rnn;
+    nw0 = L.w0[rn];
+    nw1 = L.w1[rn];
+    ncar = car_of(rn);
+    rnn = slot_of(st + 2);
     const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
     const bool pbase = valid && mq_stream(w0) == in_st;
-    const uint64_t av = AOP == 4 ? 0ull : mq_src(L, c, asrc, r, ts);
+    const uint64_t av = AOP == 4 ? 0ull : asrc == MQ_SRC_KEY ? (uint64_t)c.keyv
+                        : (asrc == MQ_SRC_TS || aw < 0) ? (uint64_t)ts : car;
     const double ad = AOP == 0 ? todouble(av, atyp) : 0.0;
     const uint64_t hcar = hk >= 4 ? mq_src(L, c, hk - 4, r, ts) : 0ull;
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       if (i >= nq) break;
-      const bool pass = pbase && ((w1 >> fbit[i]) & 1ull) != 0;
+      if (kEmit && i != qi) continue;
+      const bool pass = pbase && ((w1 >> qc[U.q0 + i].filter_bit) & 1ull) != 0;
+      const uint64_t hconst_i = qc[U.q0 + i].hav_cconst;
       const uint64_t o = acc[i];
       const bool first = cnt[i] == 0;
       cnt[i] += pass ? 1u : 0u;
@@ -856,52 +929,49 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
         nv = (first || (AOP == 2 ? lt : gt)) ? av : o;
       }
       if (AOP != 4) acc[i] = pass ? nv : o;
-      const uint64_t avgb = AOP == 0 ? from_f64(as_f64(acc[i]) / (double)(int64_t)cnt[i]) : 0ull;
+      const uint64_t avgb = (AOP == 0 && need_avg) ? from_f64(as_f64(acc[i]) / (double)(int64_t)cnt[i]) : 0ull;
       bool em = pass;
       if (hav) {
         const uint64_t hv = msel(hk == 0, (uint64_t)c.keyv,
                                  msel(hk == 1, cnt[i], msel(hk == 2, acc[i], msel(hk == 3, avgb, hcar))));
         bool lt, eq, gt;
         if (hdbl) {
-          const double x = todouble(hv, htype), y = as_f64(hconst[i]);
+          const double x = todouble(hv, htype), y = as_f64(hconst_i);
           lt = x < y; eq = x == y; gt = x > y;
         } else {
           const int64_t x = Q0.hav_ctype == T_LONG ? (int64_t)hv : (int64_t)(int32_t)hv;
-          const int64_t y = Q0.hav_ctype == T_LONG ? (int64_t)hconst[i] : (int64_t)(int32_t)hconst[i];
+          const int64_t y = Q0.hav_ctype == T_LONG ? (int64_t)hconst_i : (int64_t)(int32_t)hconst_i;
           lt = x < y; eq = x == y; gt = x > y;
         }
         em = em && (mne ? !eq : ((lt && mlt) || (eq && meq) || (gt && mgt)));
       }
       const uint64_t m = __ballot(em);
       if (kEmit && m) {
-        // the row: output pointers through the constant address space (scalar
-        // loads, no LDS round trip per column), values by the decoded kinds
-        CMqQuery& Q = qc[U.q0 + i];
-        typedef __attribute__((address_space(1))) uint64_t g64;
-        typedef __attribute__((address_space(1))) uint32_t g32;
-        typedef __attribute__((address_space(1))) uint8_t g8;
-        const unsigned long long p = curv[i] + (unsigned long long)__popcll(m & lanemask_lt());
-        if (em && (int64_t)p < Q.out_cap && !(c.ablate & 1)) {
+        const uint32_t n = (uint32_t)__popcll(m);
+        if (sc + n > scap) flush(qc[U.q0 + i]);
+        if (em) {
+          const uint32_t pos = sc + (uint32_t)__popcll(m & lanemask_lt());
           const uint32_t row = mq_row(w0);
 #pragma unroll
           for (int x = 0; x < kMqMaxSel; ++x) {
             if (x >= nsel) break;
             const int k = ckind[x];
-            const uint64_t v = k == 0 ? (uint64_t)c.keyv : k == 1 ? cnt[i] : k == 2 ? acc[i] : k == 3 ? avgb
-                               : mq_src(L, c, k - 4, r, ts);
-            if (cw[x] == 8) ((g64*)Q.out_col[x])[p] = v;
-            else if (cw[x] == 4) ((g32*)Q.out_col[x])[p] = (uint32_t)v;
-            else ((g8*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
+            stg[x * scap + pos] = k == 0 ? (uint64_t)c.keyv : k == 1 ? cnt[i] : k == 2 ? acc[i] : k == 3 ? avgb
+                                  : mq_src(L, c, k - 4, r, ts);
           }
-          ((g64*)Q.out_ts)[p] = (uint64_t)ts;
-          ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
-        } else if (em && (int64_t)p >= Q.out_cap) {
-          set_err(c.err, ERR_OUT_CAP);
+          stg[nsel * scap + pos] = (uint64_t)ts;
+          stg[(nsel + 1) * scap + pos] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
         }
+        sc += n;
       }
-      curv[i] += (unsigned long long)__popcll(m);
+      if (!kEmit) curv[i] += (unsigned long long)__popcll(m);
     }
   }
+  if (kEmit) {
+    flush(qc[U.q0 + qi]);
+    curv[qi] = opos;
+  }
+  }   // qi
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < NU; ++i)
@@ -1158,9 +1228,9 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
         // the shapes built in (the rest run mq_agg_unit): compile time and
         // code size grow with every instance
         switch (U.fast) {
-          case 1: mq_agg_fast<kE, NC, 8, 0, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
-          case 2: mq_agg_fast<kE, NC, 8, 1, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
-          default: mq_agg_fast<kE, NC, 8, 4, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
+          case 1: mq_agg_fast<kE, NC, 4, 0, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
+          case 2: mq_agg_fast<kE, NC, 4, 1, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
+          default: mq_agg_fast<kE, NC, 4, 4, 0>(L, c, U, qc, state_b, kidx, ks, maxlen, cur); break;
         }
       } else if (U.nu == 8) {
         mq_agg_unit<kE, NC, 8, 1>(L, c, U, qc, state_b, kidx, ks, maxlen, cur);
@@ -1182,16 +1252,16 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       const int b = __builtin_amdgcn_readfirstlane(it - u * nblk);
       const int q0 = units[u].q0, nqu = units[u].nq;
       for (int q = lane; q < nqu; q += 64) L.wcur[wave][q] = 0;
-      __threadfence_block();
+      wave_lds_sync();
       const uint64_t tu = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
       run_unit(std::false_type{}, u, b);
       MQ_UNIT_TICKS(0, u, tu);
-      __threadfence_block();
+      wave_lds_sync();
       for (int q = lane; q < nqu; q += 64) {
         const unsigned long long n = L.wcur[wave][q];
         L.wcur[wave][q] = n ? atomicAdd(qc[q0 + q].out_count, n) : 0ull;
       }
-      __threadfence_block();
+      wave_lds_sync();
       const uint64_t tv = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
       run_unit(std::true_type{}, u, b);
       MQ_UNIT_TICKS(1, u, tv);
