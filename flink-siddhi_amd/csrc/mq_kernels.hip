@@ -758,14 +758,12 @@ __device__ __forceinline__ uint64_t msel(bool c, uint64_t a, uint64_t b) {
 // vmcnt counts stores too).
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0f70); }
 
-// LDS written by some lanes of a wave, then read by others: the wave's LDS
-// operations complete in order, so a compiler fence plus an lgkmcnt(0) wait
-// is enough.  (__threadfence_block would also wait for every global store in
-// flight: on CDNA vmcnt counts stores.)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-}
+// LDS written by some lanes of a wave, then read by others: one wave's LDS
+// operations are performed in issue order, so only the compiler must not
+// reorder them (a wavefront-scope fence: no wait instruction).
+// __threadfence_block would also wait for every global store in flight (on
+// CDNA vmcnt counts stores).
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 // Up to NU group-by aggregations of one shape with at most one non-count
 // accumulator, its operation fixed at compile time (AOP 0: sum / avg in
@@ -843,24 +841,26 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
     for (int x = 0; x < kMqMaxSel; ++x) any = any || (x < nsel && ckind[x] == 3);
     return any;
   }();
-  // Emit pass: one query at a time, its rows staged in the wave's LDS rows
-  // (column-major, `scap` rows) and written as contiguous runs of up to scap
-  // rows per column: a step emits ~10 rows of a query, so per-step stores
-  // would write short runs of many open lines.
+  // Emit pass: each query's rows are staged in its own part of the wave's
+  // LDS rows (column-major, `scap` rows) and written as contiguous runs of up
+  // to scap rows per column (16 at three select items: whole 128-byte lines),
+  // not as the ~10 rows a step emits per query.
   const int ncols = nsel + 2;
-  const uint32_t scap = (uint32_t)(kMqStgWords / ncols);
-  uint64_t* stg = const_cast<uint64_t*>(L.stg[threadIdx.x >> 6]);
-  const int nq_outer = kEmit ? nq : 1;
-  for (int qi = 0; qi < nq_outer; ++qi) {
-  uint32_t sc = 0;                                       // staged rows
-  unsigned long long opos = kEmit ? curv[qi] : 0ull;    // output row of the first staged row
-  auto flush = [&](CMqQuery& Q) {
+  constexpr int kPart = kMqStgWords / NU;
+  const uint32_t scap = (uint32_t)(kPart / ncols);
+  uint64_t* stg0 = const_cast<uint64_t*>(L.stg[threadIdx.x >> 6]);
+  uint32_t sc[NU];                 // staged rows per query
+#pragma unroll
+  for (int i = 0; i < NU; ++i) sc[i] = 0;
+  auto flush = [&](int i) {
     typedef __attribute__((address_space(1))) uint64_t g64;
     typedef __attribute__((address_space(1))) uint32_t g32;
     typedef __attribute__((address_space(1))) uint8_t g8;
+    CMqQuery& Q = qc[U.q0 + i];
+    const uint64_t* stg = stg0 + i * kPart;
     wave_lds_sync();
-    for (uint32_t j = lane; j < sc; j += 64) {
-      const unsigned long long p = opos + j;
+    for (uint32_t j = lane; j < sc[i]; j += 64) {
+      const unsigned long long p = curv[i] + j;
       if ((int64_t)p >= Q.out_cap) {
         set_err(c.err, ERR_OUT_CAP);
         continue;
@@ -878,8 +878,8 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
       ((g64*)Q.out_seq)[p] = stg[(nsel + 1) * scap + j];
     }
     wave_lds_sync();
-    opos += sc;
-    sc = 0;
+    curv[i] += sc[i];
+    sc[i] = 0;
   };
   // The step loop is a chain of LDS reads (run slot -> record -> argument)
   // with few waves per SIMD to hide it: the next step's record is read one
@@ -912,7 +912,6 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       if (i >= nq) break;
-      if (kEmit && i != qi) continue;
       const bool pass = pbase && ((w1 >> qc[U.q0 + i].filter_bit) & 1ull) != 0;
       const uint64_t hconst_i = qc[U.q0 + i].hav_cconst;
       const uint64_t o = acc[i];
@@ -948,9 +947,34 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
       const uint64_t m = __ballot(em);
       if (kEmit && m) {
         const uint32_t n = (uint32_t)__popcll(m);
-        if (sc + n > scap) flush(qc[U.q0 + i]);
-        if (em) {
-          const uint32_t pos = sc + (uint32_t)__popcll(m & lanemask_lt());
+        if (sc[i] + n > scap) flush(i);
+        if (n > scap) {
+          // more rows than the staging part holds (rare): stored directly
+          typedef __attribute__((address_space(1))) uint64_t g64;
+          typedef __attribute__((address_space(1))) uint32_t g32;
+          typedef __attribute__((address_space(1))) uint8_t g8;
+          CMqQuery& Q = qc[U.q0 + i];
+          const unsigned long long p = curv[i] + (unsigned long long)__popcll(m & lanemask_lt());
+          if (em && (int64_t)p >= Q.out_cap) set_err(c.err, ERR_OUT_CAP);
+          if (em && (int64_t)p < Q.out_cap && !(c.ablate & 1)) {
+            const uint32_t row = mq_row(w0);
+#pragma unroll
+            for (int x = 0; x < kMqMaxSel; ++x) {
+              if (x >= nsel) break;
+              const int k = ckind[x];
+              const uint64_t v = k == 0 ? (uint64_t)c.keyv : k == 1 ? cnt[i] : k == 2 ? acc[i] : k == 3 ? avgb
+                                 : mq_src(L, c, k - 4, r, ts);
+              if (cw[x] == 8) ((g64*)Q.out_col[x])[p] = v;
+              else if (cw[x] == 4) ((g32*)Q.out_col[x])[p] = (uint32_t)v;
+              else ((g8*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
+            }
+            ((g64*)Q.out_ts)[p] = (uint64_t)ts;
+            ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
+          }
+          curv[i] += n;
+        } else if (em) {
+          uint64_t* stg = stg0 + i * kPart;
+          const uint32_t pos = sc[i] + (uint32_t)__popcll(m & lanemask_lt());
           const uint32_t row = mq_row(w0);
 #pragma unroll
           for (int x = 0; x < kMqMaxSel; ++x) {
@@ -962,16 +986,16 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
           stg[nsel * scap + pos] = (uint64_t)ts;
           stg[(nsel + 1) * scap + pos] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
         }
-        sc += n;
+        if (n <= scap) sc[i] += n;
       }
       if (!kEmit) curv[i] += (unsigned long long)__popcll(m);
     }
   }
   if (kEmit) {
-    flush(qc[U.q0 + qi]);
-    curv[qi] = opos;
+#pragma unroll
+    for (int i = 0; i < NU; ++i)
+      if (i < nq && sc[i]) flush(i);
   }
-  }   // qi
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < NU; ++i)
