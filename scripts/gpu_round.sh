@@ -1,23 +1,33 @@
 #!/bin/bash
 # The round's measurement set (results under gpurun_out/, copied to profiles/
-# by hand): bench lines for every workload, rocprofv3 kernel stats of the
-# config-3 / config-2 / Zipf benches, PMC passes of config 3, the 2-rank
-# rehearsal.  Each step has its own time limit (scripts/gpu_steps.sh).
+# by hand): bench lines for every workload, rocprofv3 kernel stats, PMC
+# passes, the GPU test suite.  Each step has its own time limit
+# (scripts/gpu_steps.sh).  usage: scripts/gpu_round.sh 1|2|3
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R="$PWD"
 PART=${1:-1}
 P="rocprofv3 --kernel-trace --stats --output-format csv -o run -d"
 if [ "$PART" = 1 ]; then
 scripts/gpu_steps.sh \
+  "450 gputest python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread" \
+  "120 smoke python -c 'import __graft_entry__ as g; g.smoke()'" \
   "300 b3 python -u bench.py" \
-  "300 s3 cd /tmp && $P $GRAFT_REPO_ROOT/gpurun_out/s3 -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu --no-parity" \
+  "300 s3 cd /tmp && $P $R/gpurun_out/s3 -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-parity" \
+  "300 b5 python -u bench.py --workload config5" \
+  "200 s5 cd /tmp && $P $R/gpurun_out/s5 -- python3 $R/bench.py --workload config5 --steps 3 --warmup 1 --no-cpu --no-parity"
+elif [ "$PART" = 2 ]; then
+scripts/gpu_steps.sh \
   "200 b2 python -u bench.py --workload filter" \
-  "200 s2 cd /tmp && $P $GRAFT_REPO_ROOT/gpurun_out/s2 -- python3 $GRAFT_REPO_ROOT/bench.py --workload filter --steps 3 --warmup 1 --no-cpu --no-parity" \
+  "200 s2 cd /tmp && $P $R/gpurun_out/s2 -- python3 $R/bench.py --workload filter --steps 3 --warmup 1 --no-cpu --no-parity" \
   "300 bz python -u bench.py --keys-dist zipf" \
-  "300 sz cd /tmp && $P $GRAFT_REPO_ROOT/gpurun_out/sz -- python3 $GRAFT_REPO_ROOT/bench.py --keys-dist zipf --steps 3 --warmup 1 --no-cpu --no-parity"
+  "200 bdo python -u bench.py --deliver --ordered --no-cpu --no-parity" \
+  "200 bd python -u bench.py --deliver --no-cpu --no-parity" \
+  "200 bh python -u bench.py --ingest host --no-cpu --no-parity" \
+  "200 sdo cd /tmp && $P $R/gpurun_out/sdo -- python3 $R/bench.py --deliver --ordered --steps 3 --warmup 1 --no-cpu --no-parity"
 else
 scripts/gpu_steps.sh \
-  "300 b5 python -u bench.py --workload config5" \
-  "200 bh python -u bench.py --ingest host --no-cpu --no-parity --deliver" \
-  "600 pmc bash scripts/gpu_pmc.sh r02_pmc.json" \
+  "400 pmc3 bash scripts/gpu_pmc.sh r03_pmc_config3.json" \
+  "300 pmc5 env BENCH_ARGS='--workload config5' PMC_EVENTS=16777216 bash scripts/gpu_pmc.sh r03_pmc_config5.json" \
+  "300 pmcf env BENCH_ARGS='--workload filter' PMC_EVENTS=100000000 bash scripts/gpu_pmc.sh r03_pmc_filter.json" \
   "600 multi bash scripts/gpu_multi_rehearsal.sh"
 fi
