@@ -45,6 +45,7 @@ __global__ void k_upper_bound(const int64_t* __restrict__ sorted, int64_t n, int
 
 constexpr int kT = 256;
 inline unsigned nblk(int64_t n) { return (unsigned)((n + kT - 1) / kT); }
+constexpr int kStatsT = 1024;   // k_seq_stats: 1024-lane blocks, one per CU
 
 // Emission order of one output stream (cep_flush, ordered_output = 1).
 // out[0] = ~min seq, out[1] = max seq (both biased by the sign bit so unsigned
@@ -63,13 +64,27 @@ __global__ void k_seq_stats(const int64_t* __restrict__ seq, const unsigned long
     hi = max(hi, b);
     desc += (i > 0 && seq[i - 1] > v) ? 1 : 0;
   }
-  // wave reduction (64 lanes), then one atomic per wave
+  // wave reduction (64 lanes), block reduction in LDS, one atomic per block
+  // and word (per-wave atomics on three words serialise: 312 us at 17.5 M rows)
   for (int o = 32; o > 0; o >>= 1) {
     lo = min(lo, (unsigned long long)__shfl_xor((long long)lo, o));
     hi = max(hi, (unsigned long long)__shfl_xor((long long)hi, o));
     desc += (unsigned long long)__shfl_xor((long long)desc, o);
   }
-  if ((threadIdx.x & 63) == 0 && n > 0) {
+  __shared__ unsigned long long red[3][kStatsT / 64];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+    red[2][w] = desc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && n > 0) {
+    for (int i = 1; i < kStatsT / 64; ++i) {
+      lo = min(lo, red[0][i]);
+      hi = max(hi, red[1][i]);
+      desc += red[2][i];
+    }
     atomicMax(&out[0], ~lo);
     atomicMax(&out[1], hi);
     if (desc) atomicAdd(&out[2], desc);
@@ -92,8 +107,8 @@ __global__ void k_seq_keys(const int64_t* __restrict__ seq, int64_t lo, int64_t 
 void launch_seq_stats(const int64_t* seq, const unsigned long long* count, int64_t cap, unsigned long long* out3,
                       hipStream_t s) {
   if (cap <= 0) return;
-  const unsigned blocks = (unsigned)std::min<int64_t>(2048, (cap + kT - 1) / kT);
-  hipLaunchKernelGGL(k_seq_stats, dim3(blocks), dim3(kT), 0, s, seq, count, cap, out3);
+  const unsigned blocks = (unsigned)std::min<int64_t>(256, (cap + kStatsT - 1) / kStatsT);
+  hipLaunchKernelGGL(k_seq_stats, dim3(blocks), dim3(kStatsT), 0, s, seq, count, cap, out3);
 }
 
 size_t order_temp_bytes(int64_t n) {
