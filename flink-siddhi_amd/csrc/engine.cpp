@@ -65,7 +65,10 @@ struct HostBuf {
 
 bool host_ensure(HostBuf* b, size_t bytes) {
   if (b->bytes >= bytes && b->p) return true;
-  const size_t nb = std::max(bytes, b->bytes * 2);
+  // pinning hundreds of MB takes ~100 ms: grow with headroom, so a delivery
+  // buffer sized by one flush's rows is not re-pinned when the next flush
+  // brings a few more
+  const size_t nb = std::max(bytes + bytes / 2, b->bytes * 2);
   if (b->p) hipHostFree(b->p);
   b->p = nullptr;
   b->bytes = 0;
