@@ -28,6 +28,5 @@ else
 scripts/gpu_steps.sh \
   "400 pmc3 bash scripts/gpu_pmc.sh r03_pmc_config3.json" \
   "300 pmc5 env BENCH_ARGS='--workload config5' PMC_EVENTS=16777216 bash scripts/gpu_pmc.sh r03_pmc_config5.json" \
-  "300 pmcf env BENCH_ARGS='--workload filter' PMC_EVENTS=100000000 bash scripts/gpu_pmc.sh r03_pmc_filter.json" \
-  "600 multi bash scripts/gpu_multi_rehearsal.sh"
+  "300 pmcf env BENCH_ARGS='--workload filter' PMC_EVENTS=100000000 bash scripts/gpu_pmc.sh r03_pmc_filter.json"
 fi
