@@ -284,6 +284,7 @@ struct MqCtx {
   const int64_t* in_seq;
   unsigned int* err;
   int ablate;
+  int32_t lg, bucket, key_stride, key_offset;   // key value of a record's key in bucket
 };
 
 // Logical carried word `src` (uniform) of window record r (MQ_SRC_*: key /
@@ -842,12 +843,12 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
     return any;
   }();
   // Emit pass: each query's rows are staged in its own part of the wave's
-  // LDS rows (column-major, `scap` rows) and written as contiguous runs of up
-  // to scap rows per column (16 at three select items: whole 128-byte lines),
-  // not as the ~10 rows a step emits per query.
-  const int ncols = nsel + 2;
+  // LDS rows and written as contiguous runs of up to scap rows per column,
+  // not as the ~10 rows a step emits per query.  A staged row is its record
+  // slot, count and accumulator (3 words whatever the select list): key, ts,
+  // seq, carried columns and the average are rebuilt from them at the flush.
   constexpr int kPart = kMqStgWords / NU;
-  const uint32_t scap = (uint32_t)(kPart / ncols);
+  constexpr uint32_t scap = (uint32_t)(kPart / 3);
   uint64_t* stg0 = const_cast<uint64_t*>(L.stg[threadIdx.x >> 6]);
   uint32_t sc[NU];                 // staged rows per query
 #pragma unroll
@@ -866,16 +867,25 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
         continue;
       }
       if (c.ablate & 1) continue;
+      const int r = (int)stg[j];
+      const uint64_t rc = stg[scap + j], ra = stg[2 * scap + j];
+      const uint64_t w0 = L.w0[r];
+      const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+      const int64_t keyv = ((((int64_t)mq_key(L.w1[r]) << c.lg) | c.bucket) * c.key_stride) + c.key_offset;
+      const uint64_t ravg = need_avg ? from_f64(as_f64(ra) / (double)(int64_t)rc) : 0ull;
 #pragma unroll
       for (int x = 0; x < kMqMaxSel; ++x) {
         if (x >= nsel) break;
-        const uint64_t v = stg[x * scap + j];
+        const int k = ckind[x];
+        const uint64_t v = k == 0 ? (uint64_t)keyv : k == 1 ? rc : k == 2 ? ra : k == 3 ? ravg
+                           : mq_src(L, c, k - 4, r, ts);
         if (cw[x] == 8) ((g64*)Q.out_col[x])[p] = v;
         else if (cw[x] == 4) ((g32*)Q.out_col[x])[p] = (uint32_t)v;
         else ((g8*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
       }
-      ((g64*)Q.out_ts)[p] = stg[nsel * scap + j];
-      ((g64*)Q.out_seq)[p] = stg[(nsel + 1) * scap + j];
+      const uint32_t row = mq_row(w0);
+      ((g64*)Q.out_ts)[p] = (uint64_t)ts;
+      ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
     }
     wave_lds_sync();
     curv[i] += sc[i];
@@ -947,7 +957,8 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
       const uint64_t m = __ballot(em);
       if (kEmit && m) {
         const uint32_t n = (uint32_t)__popcll(m);
-        if (sc[i] + n > scap) flush(i);
+        if (sc[i] + n > scap && !(c.ablate & 4)) flush(i);
+        if (c.ablate & 4) sc[i] = 0;
         if (n > scap) {
           // more rows than the staging part holds (rare): stored directly
           typedef __attribute__((address_space(1))) uint64_t g64;
@@ -972,19 +983,12 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
             ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
           }
           curv[i] += n;
-        } else if (em) {
+        } else if (em && !(c.ablate & 2)) {
           uint64_t* stg = stg0 + i * kPart;
           const uint32_t pos = sc[i] + (uint32_t)__popcll(m & lanemask_lt());
-          const uint32_t row = mq_row(w0);
-#pragma unroll
-          for (int x = 0; x < kMqMaxSel; ++x) {
-            if (x >= nsel) break;
-            const int k = ckind[x];
-            stg[x * scap + pos] = k == 0 ? (uint64_t)c.keyv : k == 1 ? cnt[i] : k == 2 ? acc[i] : k == 3 ? avgb
-                                  : mq_src(L, c, k - 4, r, ts);
-          }
-          stg[nsel * scap + pos] = (uint64_t)ts;
-          stg[(nsel + 1) * scap + pos] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
+          stg[pos] = (uint64_t)r;
+          stg[scap + pos] = cnt[i];
+          stg[2 * scap + pos] = acc[i];
         }
         if (n <= scap) sc[i] += n;
       }
@@ -1045,7 +1049,8 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
   uint64_t* const state_b = a.state + (int64_t)bucket * a.words * kpb;
   const int64_t ts_base = a.chunk_base[0], seq_base = a.chunk_base[1];
   CMqQuery* qc = (CMqQuery*)a.q;
-  const MqCtx<NC> c0{ts_base, seq_base, 0, 0, 0, a.lmap[0], a.lmap[1], a.lmap[2], a.lmap[3], a.in_seq, a.err, a.ablate};
+  const MqCtx<NC> c0{ts_base, seq_base, 0, 0, 0, a.lmap[0], a.lmap[1], a.lmap[2], a.lmap[3], a.in_seq, a.err, a.ablate,
+                        lg, bucket, a.key_stride, a.key_offset};
   MQ_STAMP(0);
   for (int q = tid; q < a.nq; q += NT) {
     MqHot& h = L.hot[q];
@@ -1174,24 +1179,25 @@ __global__ __launch_bounds__(kMqWalkThreads, 1) void k_mqwalk(MqWalkArgs a) {
       if (tid == 0) L.kstart[kpb] = tot;
     }
     lds_barrier();
+    // counting sort by key into a scratch array (the wave staging rows are
+    // free until the items run), then each record's arrival rank inside its
+    // key run (rows are unique in a chunk) places it: one short independent
+    // loop per record instead of one serial insertion sort per key
+    static_assert(W * sizeof(uint16_t) <= sizeof(L.stg), "sort scratch in the staging rows");
+    uint16_t* tmp = reinterpret_cast<uint16_t*>(&L.stg[0][0]);
     for (uint32_t p = tid; p < nw; p += NT) {
       const uint32_t slot = atomicAdd(&L.kcur[mq_key(L.w1[p])], 1u);
-      L.sorted[slot] = (uint16_t)p;
+      tmp[slot] = (uint16_t)p;
     }
     lds_barrier();
-    // arrival order inside each key run (insertion sort on the chunk row)
-    for (int k = tid; k < kpb; k += NT) {
+    for (uint32_t q = tid; q < nw; q += NT) {
+      const uint16_t e = tmp[q];
+      const uint32_t k = mq_key(L.w1[e]);
       const uint32_t q0 = L.kstart[k], q1 = L.kstart[k + 1];
-      for (uint32_t i = q0 + 1; i < q1; ++i) {
-        const uint16_t v = L.sorted[i];
-        const uint32_t rv = mq_row(L.w0[v]);
-        uint32_t j = i;
-        while (j > q0 && mq_row(L.w0[L.sorted[j - 1]]) > rv) {
-          L.sorted[j] = L.sorted[j - 1];
-          --j;
-        }
-        L.sorted[j] = v;
-      }
+      const uint32_t re = mq_row(L.w0[e]);
+      uint32_t rank = 0;
+      for (uint32_t j = q0; j < q1; ++j) rank += mq_row(L.w0[tmp[j]]) < re ? 1u : 0u;
+      L.sorted[q0 + rank] = e;
     }
     // keys by descending run length: a wave's loop runs to the longest run
     // of its 64 keys, so blocks of alike runs keep the lanes busy

@@ -81,6 +81,41 @@ def test_config5_64_queries_two_batches():
     assert seq_rows > 20 and agg_rows > 1000, (seq_rows, agg_rows)
 
 
+def test_config5_snapshot_restore_mid_stream():
+    # the multi-query group's state (bit-parallel sequence partials, running
+    # aggregates; bucket-contiguous on the device) survives a snapshot into a
+    # fresh runtime: both halves together equal one uninterrupted oracle run
+    from flink_siddhi import _lib as L
+    plan = config5_plan()
+    w = three_streams(8000, 48)
+    want = oracle_run(plan, events(w))
+    n = len(w["ts"])
+    h = n // 2 + 17
+    cols = lambda s, e: [w["k"][s:e], w["ts"][s:e], w["id"][s:e], w["price"][s:e]]  # noqa: E731
+    rt = fs.SiddhiAppRuntime(plan, key_capacity=64)
+    for o in outputs():
+        rt.add_callback(o)
+    rt.send("A", w["ts"][:h], cols(0, h), streams=w["stream"][:h])
+    rt.flush()
+    assert rt.stats().kernel_launches[L.K_MQ_WALK] > 0
+    first = {o: engine_rows(rt.collect(o)) for o in outputs()}
+    snap = rt.snapshot()
+    rt.shutdown()
+    rt2 = fs.SiddhiAppRuntime(plan, key_capacity=64)
+    for o in outputs():
+        rt2.add_callback(o)
+    rt2.restore(snap)
+    rt2.send("A", w["ts"][h:], cols(h, n), streams=w["stream"][h:])
+    rt2.flush()
+    second = {o: engine_rows(rt2.collect(o)) for o in outputs()}
+    rt2.shutdown()
+    crossing = 0
+    for o in outputs():
+        assert_same_rows(first[o] + second[o], want.get(o, []), o)
+        crossing += len(second[o])
+    assert crossing > 500
+
+
 def config5_exact_plan():
     return workload.config5_plan()
 

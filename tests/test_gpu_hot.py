@@ -185,3 +185,22 @@ def test_low_threshold_fills_every_slot(monkeypatch):
     assert st.kernel_launches[L.K_HOT] > 0
     assert st.hot_keys > 512, st.hot_keys
     assert_same_per_key(got, want)
+
+
+def test_hot_keys_come_and_go_with_overlap():
+    # CEP_OVERLAP=1 runs each chunk's partition on the side stream beside the
+    # previous chunk's walk; with hot keys the partition must also wait for
+    # the previous hot update (it reads hot_id / hot_key).  The knob is read
+    # once per process, so the case runs in one child process (the parent
+    # keeps the GPU idle meanwhile) on the come-and-go stream above.
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    here = Path(__file__).resolve().parent
+    env = dict(os.environ, CEP_OVERLAP="1")
+    code = ("import sys; sys.path[:0] = %r; import test_gpu_hot as t; "
+            "t.test_hot_keys_come_and_go(); print('overlap ok')" % [str(here), str(here.parent / "oracle"),
+                                                                     str(here.parent / "flink-siddhi_amd")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "overlap ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
