@@ -217,6 +217,7 @@ struct cep_app {
   DevBuf stamps;               // CEP_STAMPS=1: walk phase stamps (diagnostics)
   DevBuf str_hash;             // Java String.hashCode per dictionary id (dynamic routing)
   HostBuf flush_words;         // cep_flush: error word + output cursors + seq stats (pinned)
+  DevBuf out_counts;           // every output's row cursor (OutStream::count points here)
   DevBuf ostats;               // cep_flush: per output {~min seq, max seq, descents} (k_seq_stats)
   DevBuf okeys[2], oidx[2], otemp;   // cep_flush: emission-order sort scratch (shared by the outputs)
   DevBuf rr_col[kMaxCols], rr_ts, rr_stream, rr_seq;   // cep_send_rows: unpacked rows
@@ -914,14 +915,17 @@ int create_runtime(cep_app* a) {
     hipMemcpy(a->konst.p, app.konst.data(), app.konst.size() * 8, hipMemcpyHostToDevice);
   hipMemset(a->err.p, 0, 64);
   hipMemset(a->rerr.p, 0, 64);
+  // every output's row cursor in one device array: the flush reads them with
+  // one copy and resets them with one memset (64 outputs at config 5)
+  if (!dev_ensure(&a->out_counts, std::max<size_t>(app.outputs.size(), 1) * 8, a->stream, false))
+    return fail(a, CEP_E_DEVICE, "out of device memory");
+  hipMemset(a->out_counts.p, 0, std::max<size_t>(app.outputs.size(), 1) * 8);
   for (auto& sd : app.outputs) {
     OutStream o;
     o.id = sd.id;
     for (auto& at : sd.attrs) o.types.push_back(at.type);
     o.cols.resize(sd.attrs.size());
-    if (hipMalloc(&o.count, sizeof(unsigned long long)) != hipSuccess)
-      return fail(a, CEP_E_DEVICE, "out of device memory");
-    hipMemset(o.count, 0, sizeof(unsigned long long));
+    o.count = (unsigned long long*)a->out_counts.p + a->outs.size();
     a->outs.push_back(std::move(o));
   }
   {
@@ -1948,9 +1952,9 @@ void cep_destroy(cep_app* a) {
     for (auto& c : o.scols) dev_free(&c);
     dev_free(&o.sts);
     dev_free(&o.sseq);
-    if (o.count) hipFree(o.count);
   }
-  for (DevBuf* b : {&a->ostats, &a->okeys[0], &a->okeys[1], &a->oidx[0], &a->oidx[1], &a->otemp}) dev_free(b);
+  for (DevBuf* b : {&a->ostats, &a->okeys[0], &a->okeys[1], &a->oidx[0], &a->oidx[1], &a->otemp, &a->out_counts})
+    dev_free(b);
   for (auto& p : a->pats) {
     dev_free(&p.khdr);
     dev_free(&p.kslot);
@@ -2323,8 +2327,7 @@ int cep_flush(cep_app* a) {
                          (unsigned long long*)a->ostats.p + 3 * i, a->stream);
   }
   hipMemcpyAsync(fw, a->err.p, 4, hipMemcpyDeviceToHost, a->stream);
-  for (size_t i = 0; i < no; ++i)
-    hipMemcpyAsync(fw + 1 + i, a->outs[i].count, 8, hipMemcpyDeviceToHost, a->stream);
+  if (no) hipMemcpyAsync(fw + 1, a->out_counts.p, no * 8, hipMemcpyDeviceToHost, a->stream);
   if (order) hipMemcpyAsync(fst, a->ostats.p, no * 3 * 8, hipMemcpyDeviceToHost, a->stream);
   if (hipStreamSynchronize(a->stream) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "device failure during processing");
@@ -2403,9 +2406,9 @@ int cep_flush(cep_app* a) {
       rows.cols = ptrs.data();
       o.fn(o.user, &rows);
     }
-    hipMemsetAsync(o.count, 0, sizeof(unsigned long long), a->stream);
     o.bound = 0;
   }
+  if (no) hipMemsetAsync(a->out_counts.p, 0, no * 8, a->stream);
   return rc;
 }
 

@@ -53,8 +53,12 @@ typedef __attribute__((address_space(4))) const MqCond CMqCond;
 __device__ __forceinline__ void mq_load_cond(CMqCond& c, TermList* tl, int32_t (&slot)[kMaxTerms]) {
   tl->n = c.tl.n;
   tl->any = c.tl.any;
+  // only the condition's own terms (most are one comparison): copying all
+  // kMaxTerms descriptors per condition and row group was most of k_mqpart's
+  // scalar work
 #pragma unroll
   for (int i = 0; i < kMaxTerms; ++i) {
+    if (i >= tl->n) break;
     tl->t[i].col = c.tl.t[i].col;
     tl->t[i].coltype = c.tl.t[i].coltype;
     tl->t[i].aop = c.tl.t[i].aop;
