@@ -100,6 +100,9 @@ def dist_init(args):
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one node by contract: gloo (the shuffle's host-to-host count group,
+        # or the rehearsal backend) binds the loopback interface
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:

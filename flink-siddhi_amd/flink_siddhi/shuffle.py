@@ -11,6 +11,7 @@ router/DynamicPartitioner.java:43-60).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence
 
 import torch
@@ -32,17 +33,30 @@ def _count_group():
     free of a device round trip (an all-to-all of a device tensor followed by
     a readback would wait for everything queued on torch's stream)."""
     if not _COUNT_GROUP:
-        _COUNT_GROUP.append(dist.new_group(backend="gloo") if not _host_staged() else None)
+        if _host_staged() and os.environ.get("CEP_COUNT_GROUP") != "side":
+            _COUNT_GROUP.append(None)          # the default group is gloo already
+        else:
+            try:
+                _COUNT_GROUP.append(dist.new_group(backend="gloo"))
+            except Exception:                  # no usable gloo transport: counts over RCCL
+                _COUNT_GROUP.append("device")
     return _COUNT_GROUP[0]
 
 
 def exchange_counts(counts: Sequence[int], device=None) -> List[int]:
     """All-to-all of the per-owner record counts -> counts received from each
-    source (host to host: no GPU synchronisation)."""
+    source (host to host over the gloo side group: no GPU synchronisation;
+    over RCCL with a readback only if that group could not be created)."""
     world = dist.get_world_size()
-    send = torch.tensor(list(counts), dtype=torch.int64)
-    recv = torch.empty(world, dtype=torch.int64)
-    dist.all_to_all_single(recv, send, group=_count_group())
+    g = _count_group()
+    if g == "device":
+        send = torch.tensor(list(counts), dtype=torch.int64, device=device)
+        recv = torch.empty(world, dtype=torch.int64, device=device)
+        dist.all_to_all_single(recv, send)
+    else:
+        send = torch.tensor(list(counts), dtype=torch.int64)
+        recv = torch.empty(world, dtype=torch.int64)
+        dist.all_to_all_single(recv, send, group=g)
     return [int(x) for x in recv.tolist()]
 
 

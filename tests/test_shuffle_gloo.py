@@ -33,7 +33,9 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, side=False):
+    if side:   # counts over a separate gloo group, as beside RCCL on GPUs
+        os.environ["CEP_COUNT_GROUP"] = "side"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -69,12 +71,13 @@ def _rank_main(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_key_shuffle_gloo_world2_matches_single_process():
+@pytest.mark.parametrize("side", [False, True])
+def test_key_shuffle_gloo_world2_matches_single_process(side):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, side)) for r in range(world)]
     for p in procs:
         p.start()
     allout = q.get(timeout=240)
