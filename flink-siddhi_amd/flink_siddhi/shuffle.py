@@ -23,7 +23,7 @@ def _host_staged() -> bool:
     return dist.get_backend() != "nccl"
 
 
-_COUNT_GROUP = []
+_COUNT_GROUP = {}   # default process group -> its count group (a re-initialised world gets a new one)
 
 
 def _count_group():
@@ -32,15 +32,16 @@ def _count_group():
     needs host split sizes, so exchanging them host to host keeps the step
     free of a device round trip (an all-to-all of a device tensor followed by
     a readback would wait for everything queued on torch's stream)."""
-    if not _COUNT_GROUP:
+    key = id(dist.group.WORLD)
+    if key not in _COUNT_GROUP:
         if _host_staged() and os.environ.get("CEP_COUNT_GROUP") != "side":
-            _COUNT_GROUP.append(None)          # the default group is gloo already
+            _COUNT_GROUP[key] = None           # the default group is gloo already
         else:
             try:
-                _COUNT_GROUP.append(dist.new_group(backend="gloo"))
+                _COUNT_GROUP[key] = dist.new_group(backend="gloo")
             except Exception:                  # no usable gloo transport: counts over RCCL
-                _COUNT_GROUP.append("device")
-    return _COUNT_GROUP[0]
+                _COUNT_GROUP[key] = "device"
+    return _COUNT_GROUP[key]
 
 
 def exchange_counts(counts: Sequence[int], device=None) -> List[int]:
