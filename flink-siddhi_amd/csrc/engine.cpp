@@ -672,6 +672,16 @@ int build_mq_groups(cep_app* a) {
     }
     gclasses[gi].push_back(c);
   }
+  // a group of one query stays on its own PatternRT: the key shuffle entry
+  // points (cep_route_batch / cep_send_records) and v2-v4 snapshots of such
+  // apps address that runtime
+  for (size_t gi = a->mqs.size(); gi-- > 0;) {
+    if (a->mqs[gi].qs.size() >= 2) continue;
+    for (int qi : a->mqs[gi].qs) a->in_mq[qi] = 0;
+    a->mqs.erase(a->mqs.begin() + gi);
+    gclasses.erase(gclasses.begin() + gi);
+    layouts.erase(layouts.begin() + gi);
+  }
   for (size_t gi = 0; gi < a->mqs.size(); ++gi)
     for (auto& c : gclasses[gi]) {
       a->mqs[gi].classes_kind.push_back(c.kind);
@@ -1754,6 +1764,8 @@ int error_status(cep_app* a, unsigned int e) {
     return fail(a, CEP_E_CAPACITY, "more distinct partition values than key_capacity (sparse_keys)");
   if (e & ERR_KEY_RANGE)
     return fail(a, CEP_E_CAPACITY, "partition key outside [0, key_capacity) or not owned by this shard");
+  if (e & ERR_TS_SPAN)
+    return fail(a, CEP_E_ARG, "timestamps of one chunk lie more than 2^31 ms apart (lower chunk_events)");
   if (e & ERR_OUT_CAP) return fail(a, CEP_E_DEVICE, "output capacity exceeded");
   return fail(a, CEP_E_DEVICE, "device error flags " + std::to_string(e));
 }
@@ -2342,70 +2354,78 @@ int cep_flush(cep_app* a) {
       rc = fail(a, CEP_E_DEVICE, "output capacity exceeded on " + o.id + ": " + std::to_string(cnt) +
                                      " rows > " + std::to_string(o.cap));
   }
+  // Rows of every output are consumed by this flush, delivered or not: a
+  // failure part-way stops delivery, records the first error and still resets
+  // every cursor below, so a later flush never hands the same rows out again.
+  const bool want_seq = !a->opt.omit_seq;
+  auto deliver = [&](OutStream& o, size_t i, size_t n) -> int {
+    const void* src_ts = o.ts.p;
+    const void* src_seq = o.seq.p;
+    std::vector<const void*> src(o.cols.size());
+    for (size_t c = 0; c < o.cols.size(); ++c) src[c] = o.cols[c].p;
+    if (order && fst[3 * i + 2] > 0) {
+      // Siddhi's emission order (StreamOutputHandler.java:63-92 receives
+      // each completing event's matches in turn): by completing event, then
+      // pending order, which the walk already keeps contiguous per key — a
+      // stable sort on seq over the window's seq range, then one gather
+      // per column, all on the device.
+      if (n > (size_t)INT32_MAX) return fail(a, CEP_E_DEVICE, "too many rows to order in one flush");
+      const uint64_t bias = 0x8000000000000000ull;
+      const int64_t lo = (int64_t)(~fst[3 * i] ^ bias), hi = (int64_t)(fst[3 * i + 1] ^ bias);
+      const uint64_t range = (uint64_t)hi - (uint64_t)lo;
+      const int bits = range ? 64 - __builtin_clzll(range) : 1;
+      const size_t tb = order_temp_bytes((int64_t)n);
+      bool ok = dev_ensure(&a->okeys[0], n * 8, a->stream, false) && dev_ensure(&a->okeys[1], n * 8, a->stream, false) &&
+                dev_ensure(&a->oidx[0], n * 4, a->stream, false) && dev_ensure(&a->oidx[1], n * 4, a->stream, false) &&
+                dev_ensure(&a->otemp, tb, a->stream, false) && dev_ensure(&o.sts, n * 8, a->stream, false) &&
+                (!want_seq || dev_ensure(&o.sseq, n * 8, a->stream, false));
+      o.scols.resize(o.cols.size());
+      for (size_t c = 0; c < o.cols.size() && ok; ++c)
+        ok = dev_ensure(&o.scols[c], n * type_width(o.types[c]), a->stream, false);
+      if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (output ordering)");
+      if (order_sort(a->otemp.p, a->otemp.bytes, (const int64_t*)o.seq.p, (int64_t)n, lo, bits, a->okeys[0].p,
+                     a->okeys[1].p, (int32_t*)a->oidx[0].p, (int32_t*)a->oidx[1].p, a->stream) != 0)
+        return fail(a, CEP_E_DEVICE, "output ordering sort failed");
+      const int32_t* perm = (const int32_t*)a->oidx[1].p;
+      for (size_t c = 0; c < o.cols.size(); ++c) {
+        launch_gather(o.cols[c].p, o.scols[c].p, perm, 0, (int64_t)n, type_width(o.types[c]), a->stream);
+        src[c] = o.scols[c].p;
+      }
+      launch_gather(o.ts.p, o.sts.p, perm, 0, (int64_t)n, 8, a->stream);
+      src_ts = o.sts.p;
+      if (want_seq) {
+        launch_gather(o.seq.p, o.sseq.p, perm, 0, (int64_t)n, 8, a->stream);
+        src_seq = o.sseq.p;
+      }
+    }
+    // one async D2H per column into pinned buffers, one sync; the seq column
+    // only when the consumer reads it (cep_options.omit_seq)
+    o.hcols.resize(o.cols.size());
+    bool ok = host_ensure(&o.hts, n * 8) && (!want_seq || host_ensure(&o.hseq, n * 8));
+    for (size_t c = 0; c < o.cols.size() && ok; ++c) ok = host_ensure(&o.hcols[c], n * type_width(o.types[c]));
+    if (!ok) return fail(a, CEP_E_DEVICE, "out of pinned host memory (output delivery)");
+    hipMemcpyAsync(o.hts.p, src_ts, n * 8, hipMemcpyDeviceToHost, a->stream);
+    if (want_seq) hipMemcpyAsync(o.hseq.p, src_seq, n * 8, hipMemcpyDeviceToHost, a->stream);
+    for (size_t c = 0; c < o.cols.size(); ++c)
+      hipMemcpyAsync(o.hcols[c].p, src[c], n * type_width(o.types[c]), hipMemcpyDeviceToHost, a->stream);
+    if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "output delivery failed");
+    std::vector<const void*> ptrs(o.cols.size());
+    for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.hcols[c].p;
+    cep_rows rows{};
+    rows.stream_id = o.id.c_str();
+    rows.n = (int64_t)n;
+    rows.ncols = (int32_t)o.cols.size();
+    rows.ts = (const int64_t*)o.hts.p;
+    rows.seq = want_seq ? (const int64_t*)o.hseq.p : nullptr;
+    rows.cols = ptrs.data();
+    o.fn(o.user, &rows);
+    return CEP_OK;
+  };
   for (size_t i = 0; i < no; ++i) {
     auto& o = a->outs[i];
     const unsigned long long cnt = rc == CEP_OK ? fw[1 + i] : 0ull;
     a->matches_out += (int64_t)cnt;
-    if (o.fn && cnt > 0 && rc == CEP_OK) {
-      const size_t n = cnt;
-      const void* src_ts = o.ts.p;
-      const void* src_seq = o.seq.p;
-      std::vector<const void*> src(o.cols.size());
-      for (size_t c = 0; c < o.cols.size(); ++c) src[c] = o.cols[c].p;
-      if (order && fst[3 * i + 2] > 0) {
-        // Siddhi's emission order (StreamOutputHandler.java:63-92 receives
-        // each completing event's matches in turn): by completing event, then
-        // pending order, which the walk already keeps contiguous per key — a
-        // stable sort on seq over the window's seq range, then one gather
-        // per column, all on the device.
-        if (n > (size_t)INT32_MAX) return fail(a, CEP_E_DEVICE, "too many rows to order in one flush");
-        const uint64_t bias = 0x8000000000000000ull;
-        const int64_t lo = (int64_t)(~fst[3 * i] ^ bias), hi = (int64_t)(fst[3 * i + 1] ^ bias);
-        const uint64_t range = (uint64_t)hi - (uint64_t)lo;
-        const int bits = range ? 64 - __builtin_clzll(range) : 1;
-        const size_t tb = order_temp_bytes((int64_t)n);
-        bool ok = dev_ensure(&a->okeys[0], n * 8, a->stream, false) && dev_ensure(&a->okeys[1], n * 8, a->stream, false) &&
-                  dev_ensure(&a->oidx[0], n * 4, a->stream, false) && dev_ensure(&a->oidx[1], n * 4, a->stream, false) &&
-                  dev_ensure(&a->otemp, tb, a->stream, false) && dev_ensure(&o.sts, n * 8, a->stream, false) &&
-                  dev_ensure(&o.sseq, n * 8, a->stream, false);
-        o.scols.resize(o.cols.size());
-        for (size_t c = 0; c < o.cols.size() && ok; ++c)
-          ok = dev_ensure(&o.scols[c], n * type_width(o.types[c]), a->stream, false);
-        if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (output ordering)");
-        if (order_sort(a->otemp.p, a->otemp.bytes, (const int64_t*)o.seq.p, (int64_t)n, lo, bits, a->okeys[0].p,
-                       a->okeys[1].p, (int32_t*)a->oidx[0].p, (int32_t*)a->oidx[1].p, a->stream) != 0)
-          return fail(a, CEP_E_DEVICE, "output ordering sort failed");
-        const int32_t* perm = (const int32_t*)a->oidx[1].p;
-        for (size_t c = 0; c < o.cols.size(); ++c) {
-          launch_gather(o.cols[c].p, o.scols[c].p, perm, 0, (int64_t)n, type_width(o.types[c]), a->stream);
-          src[c] = o.scols[c].p;
-        }
-        launch_gather(o.ts.p, o.sts.p, perm, 0, (int64_t)n, 8, a->stream);
-        launch_gather(o.seq.p, o.sseq.p, perm, 0, (int64_t)n, 8, a->stream);
-        src_ts = o.sts.p;
-        src_seq = o.sseq.p;
-      }
-      // one async D2H per column into pinned buffers, one sync
-      o.hcols.resize(o.cols.size());
-      bool ok = host_ensure(&o.hts, n * 8) && host_ensure(&o.hseq, n * 8);
-      for (size_t c = 0; c < o.cols.size() && ok; ++c) ok = host_ensure(&o.hcols[c], n * type_width(o.types[c]));
-      if (!ok) return fail(a, CEP_E_DEVICE, "out of pinned host memory (output delivery)");
-      hipMemcpyAsync(o.hts.p, src_ts, n * 8, hipMemcpyDeviceToHost, a->stream);
-      hipMemcpyAsync(o.hseq.p, src_seq, n * 8, hipMemcpyDeviceToHost, a->stream);
-      for (size_t c = 0; c < o.cols.size(); ++c)
-        hipMemcpyAsync(o.hcols[c].p, src[c], n * type_width(o.types[c]), hipMemcpyDeviceToHost, a->stream);
-      if (hipStreamSynchronize(a->stream) != hipSuccess) return fail(a, CEP_E_DEVICE, "output delivery failed");
-      std::vector<const void*> ptrs(o.cols.size());
-      for (size_t c = 0; c < o.cols.size(); ++c) ptrs[c] = o.hcols[c].p;
-      cep_rows rows{};
-      rows.stream_id = o.id.c_str();
-      rows.n = (int64_t)n;
-      rows.ncols = (int32_t)o.cols.size();
-      rows.ts = (const int64_t*)o.hts.p;
-      rows.seq = (const int64_t*)o.hseq.p;
-      rows.cols = ptrs.data();
-      o.fn(o.user, &rows);
-    }
+    if (o.fn && cnt > 0 && rc == CEP_OK) rc = deliver(o, i, (size_t)cnt);
     o.bound = 0;
   }
   if (no) hipMemsetAsync(a->out_counts.p, 0, no * 8, a->stream);
@@ -2817,7 +2837,10 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
       }
     }
   } else if (!a->mqs.empty()) {
-    return fail(a, CEP_E_STATE, "snapshot has no multi-query group state (version < 5)");
+    // v2-v4 kept these queries on per-query runtimes: a runtime created with
+    // CEP_NO_MQ=1 has that layout and restores the snapshot
+    return fail(a, CEP_E_STATE, "snapshot has no multi-query group state (version < 5): "
+                                "create the runtime with CEP_NO_MQ=1 to restore it on per-query state");
   }
   // Phase 2: commit (device allocations first, so a failure leaves the
   // runtime as it was)

@@ -62,6 +62,7 @@ enum : uint32_t {
   ERR_WINDOW = 16u,          // bucket window logic error
   ERR_POOL = 32u,            // pending overflow pool exhausted
   ERR_KEYMAP = 64u,          // more distinct partition values than key_capacity (sparse keys)
+  ERR_TS_SPAN = 128u,        // a chunk's ts lie more than 2^31 ms either side of its first row
 };
 
 // Per-key state header: pending count (bits 0-7, <= S) | started << 8 |

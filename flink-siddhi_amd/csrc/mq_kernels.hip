@@ -211,8 +211,10 @@ __global__ __launch_bounds__(kMqPartThreads, 1) void k_mqpart(MqPartArgs a) {
         if (packed[ee] == 0xffffffffu) continue;
         const uint32_t b = packed[ee] >> 15;
         const uint32_t slot = hist[b] + (packed[ee] & 0x7fffu);
+        // ts relative to the chunk's first row, signed: rows before it are
+        // legal unless some query has `within` (checked above)
         const int64_t dts = (int64_t)tsv[e] - ts_base;
-        if (dts < 0 || dts > 0xffffffffll) set_err(a.err, ERR_ORDER);
+        if (dts < INT32_MIN || dts > INT32_MAX) set_err(a.err, ERR_TS_SPAN);
         uint64_t* gp = trecs + (int64_t)slot * RW;
         gp[0] = (uint64_t)(uint32_t)dts | ((uint64_t)(uint32_t)(r0 + 64 * ee) << 32) | ((uint64_t)sb[e] << 57);
         gp[1] = mask[e] | ((uint64_t)lkey[ee] << 48);
@@ -382,7 +384,7 @@ __device__ __forceinline__ uint32_t mq_seq(const MqLds<NC>& L, const MqCtx<NC>& 
     const int r = L.sorted[c.r0 + (valid ? i : 0u)];   // lanes past their run re-read a record
     const uint64_t w0 = L.w0[r], w1 = L.w1[r];
     const int st = mq_stream(w0);
-    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const int64_t ts = c.ts_base + (int64_t)(int32_t)(uint32_t)w0;
     const bool rel = valid && ((smask >> st) & 1u) != 0;
     auto cond = [&](int s) { return ((w1 >> ((sbit >> (6 * s)) & 63u)) & 1ull) != 0; };
     // the live partial: expired by `within`, else stays in its count state
@@ -521,7 +523,7 @@ __device__ __forceinline__ void mq_seq_bp(const MqLds<NC>& L, const MqCtx<NC>& c
     const int r = L.sorted[c.r0 + (valid ? i : 0u)];   // lanes past their run re-read a record
     const uint64_t w0 = L.w0[r], w1 = L.w1[r];
     const int st = mq_stream(w0);
-    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const int64_t ts = c.ts_base + (int64_t)(int32_t)(uint32_t)w0;
     const uint32_t s1 = valid ? ((sos >> (4 * st)) & 15u) : 0u;   // target state + 1 (0: not read)
     const bool rel = s1 != 0;
     const int s = rel ? (int)s1 - 1 : 0;
@@ -662,7 +664,7 @@ __device__ __forceinline__ void mq_agg_unit(const MqLds<NC>& L, const MqCtx<NC>&
     const bool valid = s < c.len;
     const int r = L.sorted[c.r0 + (valid ? s : 0u)];   // lanes past their run re-read a record
     const uint64_t w0 = L.w0[r], w1 = L.w1[r];
-    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const int64_t ts = c.ts_base + (int64_t)(int32_t)(uint32_t)w0;
     const bool pbase = valid && mq_stream(w0) == in_st;
     // the arguments, once for every query of the unit
     uint64_t av[NA];
@@ -874,7 +876,7 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
       const int r = (int)stg[j];
       const uint64_t rc = stg[scap + j], ra = stg[2 * scap + j];
       const uint64_t w0 = L.w0[r];
-      const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+      const int64_t ts = c.ts_base + (int64_t)(int32_t)(uint32_t)w0;
       const int64_t keyv = ((((int64_t)mq_key(L.w1[r]) << c.lg) | c.bucket) * c.key_stride) + c.key_offset;
       const uint64_t ravg = need_avg ? from_f64(as_f64(ra) / (double)(int64_t)rc) : 0ull;
 #pragma unroll
@@ -917,7 +919,7 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
     nw1 = L.w1[rn];
     ncar = car_of(rn);
     rnn = slot_of(st + 2);
-    const int64_t ts = c.ts_base + (int64_t)(uint32_t)w0;
+    const int64_t ts = c.ts_base + (int64_t)(int32_t)(uint32_t)w0;
     const bool pbase = valid && mq_stream(w0) == in_st;
     const uint64_t av = AOP == 4 ? 0ull : asrc == MQ_SRC_KEY ? (uint64_t)c.keyv
                         : (asrc == MQ_SRC_TS || aw < 0) ? (uint64_t)ts : car;

@@ -97,7 +97,8 @@ class cep_options(C.Structure):
                 ("buckets_log2", C.c_int32), ("profile", C.c_int32),
                 ("ordered_output", C.c_int32), ("key_stride", C.c_int32),
                 ("key_offset", C.c_int32), ("pending_pool_log2", C.c_int32),
-                ("sparse_keys", C.c_int32), ("late_policy", C.c_int32), ("reserved", C.c_int32 * 4)]
+                ("sparse_keys", C.c_int32), ("late_policy", C.c_int32), ("omit_seq", C.c_int32),
+                ("reserved", C.c_int32 * 3)]
 
 
 class cep_batch(C.Structure):

@@ -142,7 +142,8 @@ class SiddhiAppRuntime:
             n = r.n
             cp = (lambda x: x.copy()) if copy or fn is None else (lambda x: x)
             ts = cp(np.ctypeslib.as_array(r.ts, shape=(n,))) if n else np.zeros(0, np.int64)
-            seq = cp(np.ctypeslib.as_array(r.seq, shape=(n,))) if n else np.zeros(0, np.int64)
+            # seq is NULL under options.omit_seq (not delivered)
+            seq = cp(np.ctypeslib.as_array(r.seq, shape=(n,))) if n and r.seq else np.zeros(0, np.int64)
             cols = []
             for c, t in enumerate(types):
                 dt = np.dtype(L.NUMPY_DTYPES[t])

@@ -12,6 +12,7 @@ router/DynamicPartitioner.java:43-60).
 from __future__ import annotations
 
 import os
+import weakref
 from typing import List, Sequence
 
 import torch
@@ -23,7 +24,10 @@ def _host_staged() -> bool:
     return dist.get_backend() != "nccl"
 
 
-_COUNT_GROUP = {}   # default process group -> its count group (a re-initialised world gets a new one)
+# default process group -> its count group.  Keyed weakly on the group
+# object itself: a destroyed world's entry goes with it, and a re-initialised
+# world (whose id() may repeat) gets a group of its own.
+_COUNT_GROUP = weakref.WeakKeyDictionary()
 
 
 def _count_group():
@@ -31,17 +35,22 @@ def _count_group():
     are host integers already (the route returns them), and RCCL's alltoallv
     needs host split sizes, so exchanging them host to host keeps the step
     free of a device round trip (an all-to-all of a device tensor followed by
-    a readback would wait for everything queued on torch's stream)."""
-    key = id(dist.group.WORLD)
-    if key not in _COUNT_GROUP:
-        if _host_staged() and os.environ.get("CEP_COUNT_GROUP") != "side":
-            _COUNT_GROUP[key] = None           # the default group is gloo already
+    a readback would wait for everything queued on torch's stream).
+
+    `dist.new_group` is a collective: if it fails, it fails on the rank that
+    raises and leaves the others blocked, so there is no per-rank fallback —
+    the error propagates (CEP_COUNT_GROUP=device selects the RCCL counts on
+    every rank instead, a choice all ranks make alike)."""
+    world = dist.group.WORLD
+    if world not in _COUNT_GROUP:
+        mode = os.environ.get("CEP_COUNT_GROUP", "")
+        if mode == "device":
+            _COUNT_GROUP[world] = "device"
+        elif _host_staged() and mode != "side":
+            _COUNT_GROUP[world] = None          # the default group is gloo already
         else:
-            try:
-                _COUNT_GROUP[key] = dist.new_group(backend="gloo")
-            except Exception:                  # no usable gloo transport: counts over RCCL
-                _COUNT_GROUP[key] = "device"
-    return _COUNT_GROUP[key]
+            _COUNT_GROUP[world] = dist.new_group(backend="gloo")
+    return _COUNT_GROUP[world]
 
 
 def exchange_counts(counts: Sequence[int], device=None) -> List[int]:

@@ -108,7 +108,11 @@ typedef struct cep_options {
                               reference hands late rows to Siddhi out of order
                               (AbstractSiddhiOperator.java:238-245); `within` and sequences
                               need event-time order, so the engine never processes them. */
-  int32_t reserved[4];
+  int32_t omit_seq;        /* 1: cep_rows.seq is NULL in callbacks and the seq column is not
+                              copied to the host (StreamOutputHandler.receive,
+                              operator/StreamOutputHandler.java:63-92, never reads it;
+                              saves 8 B per delivered row); 0: delivered (default) */
+  int32_t reserved[3];
 } cep_options;
 
 /* Fill *opt with defaults. */
