@@ -1452,7 +1452,9 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     }
     {
       LaunchTimer t(a, CEP_K_CF_WALK);
-      launch_cf_walk(wa, P, a->stream);
+      static const bool walk1 = std::getenv("CEP_CF_WALK") && std::atoi(std::getenv("CEP_CF_WALK")) == 1;
+      if (walk1 || wa.stamps) launch_cf_walk(wa, P, a->stream);   // stamps: k_cfwalk's phase diagnostics
+      else launch_cf_walk2(wa, P, a->stream);
     }
     if (hot) {
       if (divert && !hot_serial) hipStreamWaitEvent(a->stream, rt.hot_join, 0);
