@@ -21,7 +21,8 @@
 //      its output rows (one atomic per wave), emits them and commits its keys'
 //      pending lists — waves never wait for each other inside a window.
 // k_cfwalk (cf_kernels.hip) does the same work with ~11 workgroup barriers
-// per window and no prefetch; CEP_CF_WALK=1 selects it.
+// per window and no prefetch; it stays the default until this build beats
+// it (CEP_CF_WALK=2 selects this one).
 #include <hip/hip_runtime.h>
 
 #include "dev_common.h"
@@ -48,6 +49,22 @@ static_assert(kOwners * 64 == kCfMaxKeys, "one owner wave per 64 keys of a bucke
 template <int NW>
 constexpr int w2_window() { return NW > 1 ? (W2_WIN > 1024 ? 1024 : W2_WIN) : W2_WIN; }
 
+// Diagnostics (CEP_STAMPS=1): s_memtime at point i of block b (wave 0), per
+// block 16 slots: 0 start, 1 setup done, window 0: 2 phase A, 3 barrier 1,
+// 4 phase B, 5 barrier 2 + prefetch issue, 6 C1 sort, 7 C2 / C3, 8 C4
+// reservation, 9 C5 key lanes, 10 C6 emission, 11 barrier 3; window 1: 12
+// barrier 1, 13 barrier 2, 14 phase C; 15 kernel end.
+#define W2_STAMP(i)                                                                 \
+  do {                                                                              \
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096)                          \
+      a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+#define W2_STAMPW(w, i0, i1)                                                        \
+  do {                                                                              \
+    if ((w) == 0) W2_STAMP(i0);                                                     \
+    else if ((w) == 1 && (i1) >= 0) W2_STAMP(i1);                                   \
+  } while (0)
+
 __device__ __forceinline__ uint32_t w2_row(uint64_t w0) { return (uint32_t)(w0 >> 32) & 0x1fffu; }
 __device__ __forceinline__ uint32_t w2_role(uint64_t w0) { return (uint32_t)(w0 >> 45) & 0x7u; }
 __device__ __forceinline__ uint32_t w2_key(uint64_t w0) { return (uint32_t)(w0 >> 48); }
@@ -57,13 +74,17 @@ __device__ __forceinline__ uint32_t w2_key(uint64_t w0) { return (uint32_t)(w0 >
 // reorder them (mq_kernels.hip wave_lds_sync).
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
+// Inclusive scan over the 64 lanes with DPP row shifts and row broadcasts
+// (VALU-only: no LDS round trip per step, unlike __shfl_up).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  // within each row of 16 lanes: shifts 1, 2, 4, 8 (lanes without a source add 0)
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  // across rows: lane 15 into rows 1 and 3, then lane 31 into rows 2 and 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
   return x;
 }
 
@@ -142,6 +163,8 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
   const int64_t ts_base = a.chunk_base[0];
   const int64_t seq_base = a.chunk_base[1];
   const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
+  W2_STAMP(0);
+  int wi = 0;   // window index (diagnostic stamps)
 
   // ---- key lane (tid < kpb; key = tid = 64 * wave + lane): pending count +
   // slots 0 / 1 in registers for the whole launch (as k_cfwalk).  A hot key's
@@ -246,10 +269,12 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
     return;
 #endif
     unsigned long long best = 0;
-    if (tb + TPT <= ts) return;   // all of this thread's tiles lie before the window
+    int tbv = tb;
+    asm volatile("" : "+v"(tbv));   // per-tile constants are recomputed, not hoisted and held
+    if (tbv + TPT <= ts) return;   // all of this thread's tiles lie before the window
 #pragma unroll
     for (int i = 0; i < TPT; ++i) {
-      const int t = tb + i + 1;
+      const int t = tbv + i + 1;
       const uint32_t sg = L.tseg[i + 1][tid];
       if (t > ts && t <= ntiles && sg <= lim) best = ((unsigned long long)t << 32) | sg;
     }
@@ -260,10 +285,12 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
 #ifdef W2_NO_BW
     return;
 #endif
-    if (tb + TPT <= t0 || tb >= t1) return;
+    int tbv = tb;
+    asm volatile("" : "+v"(tbv));
+    if (tbv + TPT <= t0 || tbv >= t1) return;
 #pragma unroll 1
     for (int i = 0; i < TPT; ++i) {
-      const int t = tb + i;
+      const int t = tbv + i;
       if (t < t0 || t >= t1) continue;
       const uint32_t s0 = L.tseg[i][tid], s1 = L.tseg[i + 1][tid];
       const uint32_t g0 = (uint32_t)t * (uint32_t)kCfTile + ((L.tlop[i >> 1][tid] >> (16 * (i & 1))) & 0xffffu) - s0;
@@ -271,6 +298,7 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
     }
   };
   lds_barrier();   // bound[] zeroed (bscan's barriers ordered the rest)
+  W2_STAMP(1);
 
   // ---- window state (uniform)
   int t0 = 0, t1 = 0;          // whole-tile window [t0, t1), or the oversize tile t0
@@ -395,7 +423,9 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
     const int nts = over ? t0 + 1 : t1;
     const uint32_t nwb = wb + nw;
     if (!more_pieces && nwb < nall) propose(nts, nwb + (uint32_t)WIN, wpar ^ 1);
+    W2_STAMPW(wi, 2, -1);
     lds_barrier();   // #1
+    W2_STAMPW(wi, 3, 12);
 
     // ================= phase B: owner ranges, next window's record table
     uint32_t os, oe;
@@ -431,25 +461,18 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
         build_wrec(nts, nt1, nwb, buf ^ 1);
       }
     }
+    W2_STAMPW(wi, 4, -1);
     lds_barrier();   // #2
 
-    // ================= phase C0: the next window's records in flight
+#ifdef W2_NOPREF   // experiment: no prefetch (the next window loads at its start)
+    const bool next_pref = false;
+#else
     const bool next_pref = !next_over && !next_none;
-    if (next_pref) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const uint32_t q = tid + i * NT;
-        if (q < nnw) {
-          wq[i] = L.wrec[buf ^ 1][q];
-          const uint64_t* r = a.recs + (int64_t)wq[i] * RW;
-          x[i] = gload4(r);
-          if (NW > 1) y[i] = r[2];
-        }
-      }
-    }
+#endif
 
     // ================= phase C: this wave's keys, no workgroup barrier
     const uint32_t nl = oe - os;   // records of this wave's keys (uniform)
+    W2_STAMPW(wi, 5, 13);
 #ifndef W2_NO_C
     // C1: counting sort by key, then arrival order inside each key run
     L.wk[wave][lane] = 0;
@@ -480,6 +503,7 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       L.ent[os + r0 + ar] = en;
     }
     wsync();
+    W2_STAMPW(wi, 6, -1);
     // C2: key lane: next B of every record (backward over the run), first /
     // last B, last A
     const uint32_t r0 = os + kst, r1 = r0 + kc;
@@ -501,29 +525,54 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
         fbs = (uint16_t)e_slot(en);
       }
     }
-    // C3: key lane: carried partials completed by the run's first B
+    if (a.stamps && (a.ablate & 256) && klane && kc > 0) {   // diagnostics: list lengths of active keys
+      unsigned long long* c = (unsigned long long*)&a.stamps[4095 * 16];
+      atomicAdd(&c[0], 1ull);
+      if (n > 2) atomicAdd(&c[1], 1ull);
+      if (n > 4) atomicAdd(&c[2], 1ull);
+      if (n > 6) atomicAdd(&c[3], 1ull);
+      if (n > 8) atomicAdd(&c[4], 1ull);
+      if (__ballot(n > 2) && lane == __ffsll((long long)__ballot(klane && kc > 0)) - 1) atomicAdd(&c[5], 1ull);
+      if (__ballot(n > 4) && lane == __ffsll((long long)__ballot(klane && kc > 0)) - 1) atomicAdd(&c[6], 1ull);
+      if (lane == __ffsll((long long)__ballot(klane && kc > 0)) - 1) atomicAdd(&c[7], 1ull);
+    }
+    // C3: key lane: carried partials completed by the run's first B.  Lists of
+    // at most two partials (the common case) are decided from registers: no
+    // global load in this phase may wait for the next window's loads.
     int cfirst = 0, cm = 0;
     uint64_t e00 = 0, e01 = 0, e10 = 0, e11 = 0;
+    auto within_of = [&](int64_t d) { return W < 0 || (d < 0 ? -d : d) <= W; };
     if (klane && kc > 0 && fbs != kNoSlot && n > 0) {
       const int64_t tbs = ts_base + (int64_t)L.rts[fbs];
-      cfirst = n;
-      for (int j = 0; j < n; ++j) {
-        const int64_t d = tbs - (int64_t)slot_word(j, 0);
-        if (W < 0 || (d < 0 ? -d : d) <= W) {
-          cfirst = j;
-          break;
+      if (n <= 2 && !(a.ablate & 16)) {
+        const bool w0 = within_of(tbs - (int64_t)t0r);
+        const bool w1 = n > 1 && within_of(tbs - (int64_t)t1r);
+        cfirst = w0 ? 0 : (w1 ? 1 : n);
+        cm = n - cfirst;
+        e00 = cfirst == 0 ? a0c0 : a1c0;
+        e01 = cfirst == 0 ? a0c1 : a1c1;
+        e10 = a1c0;
+        e11 = a1c1;
+      } else {
+        cfirst = n;
+        for (int j = 0; j < n; ++j) {
+          if (within_of(tbs - (int64_t)slot_word(j, 0))) {
+            cfirst = j;
+            break;
+          }
+        }
+        cm = n - cfirst;
+        if (cm > 0) {
+          e00 = c1 ? slot_word(cfirst, 2) : 0ull;
+          e01 = c2 ? slot_word(cfirst, 3) : 0ull;
+        }
+        if (cm > 1) {
+          e10 = c1 ? slot_word(cfirst + 1, 2) : 0ull;
+          e11 = c2 ? slot_word(cfirst + 1, 3) : 0ull;
         }
       }
-      cm = n - cfirst;
-      if (cm > 0) {
-        e00 = c1 ? slot_word(cfirst, 2) : 0ull;
-        e01 = c2 ? slot_word(cfirst, 3) : 0ull;
-      }
-      if (cm > 1) {
-        e10 = c1 ? slot_word(cfirst + 1, 2) : 0ull;
-        e11 = c2 ? slot_word(cfirst + 1, 3) : 0ull;
-      }
     }
+    W2_STAMPW(wi, 7, -1);
     wsync();   // nextb written by key lanes, read by position lanes below
     // C4: output rows per sorted position (record matches + carried matches
     // at the run start), one reservation per wave
@@ -537,10 +586,8 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       uint32_t val = 0;
       if (e < nl) {
         const uint16_t nb = L.nextb[os + e];
-        if ((e_role(en) & ROLE_A) && nb != kNoSlot) {
-          const int64_t d = (int64_t)L.rts[nb] - (int64_t)L.rts[e_slot(en)];
-          val = (W < 0 || (d < 0 ? -d : d) <= W) ? 1u : 0u;
-        }
+        if ((e_role(en) & ROLE_A) && nb != kNoSlot)
+          val = within_of((int64_t)L.rts[nb] - (int64_t)L.rts[e_slot(en)]) ? 1u : 0u;
         if (e == kstk) val += (uint32_t)cmk;
       }
       const uint32_t incl = wave_incl_scan(val);
@@ -550,10 +597,11 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
     unsigned long long obase = 0;
     if (lane == 0 && rows) obase = atomicAdd(a.out.count, (unsigned long long)rows);
     obase = __shfl(obase, 0, 64);
+#endif
+#ifndef W2_NO_C
+    W2_STAMPW(wi, 8, -1);
     wsync();   // vout
-    // C5: key lane: carried rows, survivors, state commit (before the record
-    // rows: a slot load issued after a wave's output stores waits for them)
-#ifndef W2_NO_C5
+    // C5: key lane: carried rows, survivors, state commit
     if (klane && kc > 0) {
       const int64_t kl = ((int64_t)tid << lg) | bucket;
       const int64_t kv = kl * p.key_stride + p.key_offset;
@@ -561,14 +609,14 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
         const int64_t bts = ts_base + (int64_t)L.rts[fbs];
         const uint64_t b0 = NW > 0 ? L.rcap[0][fbs] : 0ull, b1 = NW > 1 ? L.rcap[NW > 1 ? 1 : 0][fbs] : 0ull;
         const unsigned long long rb = obase + L.vout[r0];
-        for (int j = 0; j < cm; ++j) {
-          const int js = cfirst + j;
-          const uint64_t x0 = j == 0 ? e00 : (j == 1 ? e10 : (c1 ? slot_word(js, 2) : 0ull));
-          const uint64_t x1 = j == 0 ? e01 : (j == 1 ? e11 : (c2 ? slot_word(js, 3) : 0ull));
+        const int64_t bseq = seq_base + (int64_t)L.rseq[fbs];
 #ifndef W2_NO_EMIT
-          w2_emit<KR>(a, rb + j, kv, x0, x1, b0, b1, bts, seq_base + (int64_t)L.rseq[fbs]);
+        w2_emit<KR>(a, rb, kv, e00, e01, b0, b1, bts, bseq);
+        if (cm > 1) w2_emit<KR>(a, rb + 1, kv, e10, e11, b0, b1, bts, bseq);
+        for (int j = 2; j < cm; ++j)   // long lists: slots in HBM (rare)
+          w2_emit<KR>(a, rb + j, kv, c1 ? slot_word(cfirst + j, 2) : 0ull, c2 ? slot_word(cfirst + j, 3) : 0ull, b0,
+                      b1, bts, bseq);
 #endif
-        }
       }
       const bool prune = W >= 0 && hasa;
       const int64_t last_a_ts = ts_base + (int64_t)last_a;
@@ -613,15 +661,28 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
         dirty = true;
       };
       if (lbp == kNoPos) {
-        int drop = 0;
-        while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
-        if (drop == 0 && cap <= S) {
-          nn = n;   // unchanged, in place
+        if (n <= 2 && !(a.ablate & 32)) {   // registers only
+          const bool d0 = n > 0 && prune && last_a_ts - (int64_t)t0r > W;
+          const bool d1 = d0 && n > 1 && prune && last_a_ts - (int64_t)t1r > W;
+          const int drop = d0 ? (d1 ? 2 : 1) : 0;
+          if (drop == 0 && cap <= S) {
+            nn = n;
+          } else {
+            const uint64_t s1t = t1r, s1a = a1c0, s1b = a1c1;
+            if (drop == 0 && n > 0) put_slot(t0r, a0c0, a0c1);
+            if (drop <= 1 && n > 1) put_slot(s1t, s1a, s1b);
+          }
         } else {
-          for (int j = drop; j < n; ++j) {
-            const uint64_t ts = slot_word(j, 0);
-            const uint64_t x0 = c1 ? slot_word(j, 2) : 0ull, x1 = c2 ? slot_word(j, 3) : 0ull;
-            put_slot(ts, x0, x1);
+          int drop = 0;
+          while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
+          if (drop == 0 && cap <= S) {
+            nn = n;   // unchanged, in place
+          } else {
+            for (int j = drop; j < n; ++j) {
+              const uint64_t ts = slot_word(j, 0);
+              const uint64_t x0 = c1 ? slot_word(j, 2) : 0ull, x1 = c2 ? slot_word(j, 3) : 0ull;
+              put_slot(ts, x0, x1);
+            }
           }
         }
       }
@@ -645,8 +706,27 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       if (nn > S) ovo = noff | kOvoWr;
       n = nn;
     }
+    W2_STAMPW(wi, 9, -1);
 #endif
-    // C6: record matches, lane per sorted position
+    // ================= C0: the next window's records go out only now: from
+    // here on this wave issues stores only, so nothing waits for these loads
+    // until the next window's phase A (vmcnt counts loads and stores in issue
+    // order: the reservation atomic and the key lanes' slot loads above would
+    // wait for them)
+    if (next_pref) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t q = tid + i * NT;
+        if (q < nnw) {
+          wq[i] = L.wrec[buf ^ 1][q];
+          const uint64_t* r = a.recs + (int64_t)wq[i] * RW;
+          x[i] = gload4(r);
+          if (NW > 1) y[i] = r[2];
+        }
+      }
+    }
+#ifndef W2_NO_C
+    // C6: record matches, lane per sorted position (stores only)
     for (uint32_t e0 = 0; e0 < nl; e0 += 64) {
       const uint32_t e = e0 + lane;
       const uint32_t en = e < nl ? L.ent[os + e] : 0u;
@@ -657,8 +737,7 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       const uint16_t nb = L.nextb[os + e];
       if (nb == kNoSlot) continue;
       const uint32_t sl = e_slot(en);
-      const int64_t d = (int64_t)L.rts[nb] - (int64_t)L.rts[sl];
-      if (W >= 0 && (d < 0 ? -d : d) > W) continue;
+      if (!within_of((int64_t)L.rts[nb] - (int64_t)L.rts[sl])) continue;
       const int64_t ats = ts_base + (int64_t)L.rts[sl];
       const int64_t bts = ts_base + (int64_t)L.rts[nb];
       const uint64_t a0 = NW > 0 ? L.rcap[0][sl] : 0ull, a1 = NW > 1 ? L.rcap[NW > 1 ? 1 : 0][sl] : 0ull;
@@ -672,11 +751,13 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
                   seq_base + (int64_t)L.rseq[nb]);
 #endif
     }
-
 #endif
+    W2_STAMPW(wi, 10, 14);
     // ================= window end: the next window
     if (tid == 0) L.bound[wpar] = 0ull;   // read in the previous window's phase B
     lds_barrier();   // #3: LDS arrays are reused
+    W2_STAMPW(wi, 11, -1);
+    ++wi;
     if (next_none) break;
     if (over && more_pieces) {
       piece += nw;
@@ -695,12 +776,13 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       t0 = nts;
       t1 = nt1;
       nw = nnw;
-      pref = true;
+      pref = next_pref;
       buf ^= 1;
     }
     wpar ^= 1;
   }
 
+  W2_STAMP(15);
   // ---- hot-key candidates: keys that made this bucket long (hot.hip)
   if (klane && a.hot_thresh && kcnt > a.hot_thresh) {
     const uint32_t key = (uint32_t)(((int64_t)tid << lg) | bucket);

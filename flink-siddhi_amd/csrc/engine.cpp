@@ -1014,6 +1014,13 @@ int create_runtime(cep_app* a) {
         p.cap_state[i] = q.ncaps[i].state;
         p.cap_index[i] = q.ncaps[i].index;
         p.cap_word[i] = q.ncaps[i].word;
+        // Siddhi reads an unmatched (optional) state's attribute as null: for
+        // a STRING the engine writes dictionary id -1, which no string has
+        const int st = q.nstates[q.ncaps[i].state].stream;
+        const int col = q.ncaps[i].word < (int)q.rec_cols_a.size() ? q.rec_cols_a[q.ncaps[i].word] : -1;
+        const bool str = st >= 0 && st < (int)app.inputs.size() && col >= 0 &&
+                         col < (int)app.inputs[st].attrs.size() && app.inputs[st].attrs[col].type == T_STRING;
+        p.cap_null[i] = str ? ~0ull : 0ull;
       }
     }
     // NFA patterns stage advanced partials in a second bank of S slots
@@ -1452,9 +1459,10 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     }
     {
       LaunchTimer t(a, CEP_K_CF_WALK);
-      static const bool walk1 = std::getenv("CEP_CF_WALK") && std::atoi(std::getenv("CEP_CF_WALK")) == 1;
-      if (walk1 || wa.stamps) launch_cf_walk(wa, P, a->stream);   // stamps: k_cfwalk's phase diagnostics
-      else launch_cf_walk2(wa, P, a->stream);
+      // k_cfwalk unless CEP_CF_WALK=2 selects the owner-wave walk (cf_walk.hip)
+      static const bool walk2 = std::getenv("CEP_CF_WALK") && std::atoi(std::getenv("CEP_CF_WALK")) == 2;
+      if (walk2) launch_cf_walk2(wa, P, a->stream);
+      else launch_cf_walk(wa, P, a->stream);
     }
     if (hot) {
       if (divert && !hot_serial) hipStreamWaitEvent(a->stream, rt.hot_join, 0);
@@ -1908,12 +1916,32 @@ void cep_destroy(cep_app* a) {
       if (!dur.empty()) std::fprintf(stderr, " median=%llu", (unsigned long long)dur[dur.size() / 2].first);
       std::fprintf(stderr, "\n");
     }
+    {   // every stamp against the previous one (both kernels' layouts)
+      double dsum[16] = {0};
+      int dn[16] = {0};
+      for (int b = 0; b < nb; ++b) {
+        const uint64_t* t = &st[(size_t)b * 16];
+        for (int i = 1; i < 16; ++i)
+          if (t[i] && t[i - 1]) {
+            dsum[i] += (double)(t[i] - t[i - 1]);
+            ++dn[i];
+          }
+      }
+      std::fprintf(stderr, "[cep stamps] walk deltas ticks/block:");
+      for (int i = 1; i < 16; ++i) std::fprintf(stderr, " d%d=%.0f(%d)", i, dn[i] ? dsum[i] / dn[i] : 0.0, dn[i]);
+      std::fprintf(stderr, "\n");
+    }
     std::fprintf(stderr, "[cep stamps] walk window0 ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);
     std::fprintf(stderr, "\n[cep stamps] walk window1 (%d blocks):", n1);
     for (int i = 10; i < 16; ++i) std::fprintf(stderr, " p%d=%.0f", i - 8, n1 ? sum[i] / n1 : 0.0);
     std::fprintf(stderr, "\n");
     const uint64_t* c = &st[(size_t)4095 * 16];
+    if (nb <= 4095 && c[0] && !c[5 + 8])
+      std::fprintf(stderr, "[cep counters] walk2 active keys=%llu n>2=%llu n>4=%llu n>6=%llu n>8=%llu | waves: n>2=%llu n>4=%llu of %llu\n",
+                   (unsigned long long)c[0], (unsigned long long)c[1], (unsigned long long)c[2],
+                   (unsigned long long)c[3], (unsigned long long)c[4], (unsigned long long)c[5],
+                   (unsigned long long)c[6], (unsigned long long)c[7]);
     if (nb <= 4095 && (c[5] || c[7]))
       std::fprintf(stderr, "[cep counters] walk: carried=%llu all=%llu keylanes_n>2=%llu drop_n>2=%llu "
                    "slot_st>=2=%llu windows=%llu keylanes=%llu\n",

@@ -128,6 +128,7 @@ struct PatternArgs {
   int32_t st_tail_opt[kMaxStates]; // every state after j is optional (min 0)
   int32_t key_col_s[8];            // partition key column per input handle
   int32_t cap_state[kMaxCaps], cap_index[kMaxCaps], cap_word[kMaxCaps];
+  uint64_t cap_null[kMaxCaps];      // a capture of a state that never matched: 0, or id -1 (null) for STRING
 };
 
 // Fast partition path: every column the pattern reads (key, f / g term

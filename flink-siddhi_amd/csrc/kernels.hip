@@ -1380,7 +1380,7 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
         started = true;
         uint64_t* ns = NSLOT(S + nf);
         ns[0] = (uint64_t)ts;
-        for (int x = 2; x < sw; ++x) ns[x * ks] = 0;
+        for (int x = 2; x < sw; ++x) ns[x * ks] = p.cap_null[x - 2];
         nfa_collect(p, ns, ks, 0, 1, rec);
         if (N == 1) {
           nfa_emit<kVm>(a, R, ns, rec, ts_base, seq_base, kl);
@@ -1429,7 +1429,7 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
         } else {
           uint64_t* ns = NSLOT(m);
           ns[0] = (uint64_t)ts;
-          for (int x = 2; x < sw; ++x) ns[x * ks] = 0;
+          for (int x = 2; x < sw; ++x) ns[x * ks] = p.cap_null[x - 2];
           nfa_collect(p, ns, ks, 0, 1, rec);
           if (settle(ns, 0, 1, rec)) ++m;
         }
