@@ -41,7 +41,7 @@ static_assert(kOwners * 64 == kCfMaxKeys, "one owner wave per 64 keys of a bucke
 // Records per window, and the waves per SIMD the register budget is set for
 // (4: two workgroups per CU, 128 VGPRs).
 #ifndef W2_WIN
-#define W2_WIN 1280
+#define W2_WIN 1024
 #endif
 #ifndef W2_MINW
 #define W2_MINW 4
@@ -94,7 +94,13 @@ __device__ __forceinline__ uint32_t e_slot(uint32_t e) { return e & 0x7ffu; }
 __device__ __forceinline__ uint32_t e_key(uint32_t e) { return (e >> 11) & 63u; }
 __device__ __forceinline__ uint32_t e_role(uint32_t e) { return (e >> 17) & 7u; }
 
-template <int NW, int WIN>
+// Per owner wave: a window's copy of its keys' pending slots 2 .. S-1 (ts,
+// captures), loaded with independent loads at the window's start, so the key
+// lanes never wait on a dependent global load in phase C (at config 3 a
+// quarter of the active keys hold more than two partials).
+constexpr int kW2Scr = 64;   // slots per wave
+
+template <int NW, int WIN, int NC>
 struct W2Lds {
   uint32_t wrec[2][WIN];                   // arena record index per window slot (this window / the next)
   uint32_t rts[WIN];                       // by slot: ts - chunk ts base
@@ -112,6 +118,9 @@ struct W2Lds {
   uint32_t obits[kCfTile / 32];            // oversize segment: tile-row presence bitmap
   uint16_t opre[kCfTile / 32];             // oversize segment: popcount prefix per bitmap word
   uint32_t scratch[kCfWalkThreads / 64 + 1];
+  uint64_t scr[kOwners][kW2Scr * (1 + NC)];   // [wave][slot * (1 + NC) + word]
+  uint32_t wrows[kOwners];                 // output rows of each owner wave (this window)
+  unsigned long long wbase[kOwners];       // their first output row
 };
 
 // One output row (as k_cfwalk's cf_emit).
@@ -147,7 +156,7 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
   constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
   constexpr int PER = (WIN + NT - 1) / NT;   // window slots per thread
   static_assert(WIN <= 2048, "entry slot field is 11 bits");
-  __shared__ W2Lds<NW, WIN> L;
+  __shared__ W2Lds<NW, WIN, NC> L;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   const PatternArgs& p = a.pat;
@@ -229,9 +238,11 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
     if (c1) a1c0 = sl_ld(1, 2);
     if (c2) a1c1 = sl_ld(1, 3);
   }
+  int scb = -1;   // this window's scratch copy of slots 2 .. min(n, S) - 1 (slot index base), or -1
   auto slot_word = [&](int j, int w) -> uint64_t {
     if (j >= 2) {
       if (j >= S) return ovp()[(int64_t)(j - S) * sw + w];
+      if (scb >= 0) return L.scr[wave][(scb + j - 2) * (1 + NC) + (w == 0 ? 0 : w - 1)];
       return sl_ld(j, w);
     }
     const uint64_t m0 = 0ull - (uint64_t)(j == 0), m1 = ~m0;
@@ -384,6 +395,32 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       }
     }
 
+    // ================= scratch: key lanes' slots 2 .. min(n, S) - 1, loads
+    // issued before this window's records are waited for (they overlap)
+    {
+      const int need = (klane && n > 2) ? min(n, S) - 2 : 0;
+      const uint32_t incl = wave_incl_scan((uint32_t)need);
+      const int off = (int)(incl - (uint32_t)need);
+      scb = (need > 0 && off + need <= kW2Scr) ? off : -1;
+      if (scb >= 0) {
+        for (int j0 = 0; j0 < need; j0 += 4) {
+          uint64_t v[4][1 + NC];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool ok = j0 + u < need;
+            v[u][0] = ok ? sl_ld(2 + j0 + u, 0) : 0ull;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[u][1 + c] = ok ? sl_ld(2 + j0 + u, 2 + c) : 0ull;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (j0 + u < need) {
+#pragma unroll
+              for (int c = 0; c <= NC; ++c) L.scr[wave][(scb + j0 + u) * (1 + NC) + c] = v[u][c];
+            }
+        }
+      }
+    }
     // ================= phase A: records -> LDS by slot, owner counts, next extent
     uint32_t own[PER], rk[PER], entv[PER];
     {
@@ -594,30 +631,33 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       if (e < nl) L.vout[os + e] = rows + incl - val;
       rows += __shfl(incl, 63, 64);
     }
-    unsigned long long obase = 0;
-    if (lane == 0 && rows) obase = atomicAdd(a.out.count, (unsigned long long)rows);
-    obase = __shfl(obase, 0, 64);
+    if (lane == 0) L.wrows[wave] = rows;
 #endif
+    // ================= the window's output reservation: one atomic per
+    // workgroup (one per wave on the single output cursor serialises every
+    // wave of the chip); the key lanes' commit runs while it is in flight
+    lds_barrier();   // #C: every wave's row count
+    if (tid == 0) {
+      unsigned long long tot = 0;
+#pragma unroll
+      for (int w = 0; w < kOwners; ++w) tot += L.wrows[w];
+      unsigned long long b = tot ? atomicAdd(a.out.count, tot) : 0ull;
+#pragma unroll
+      for (int w = 0; w < kOwners; ++w) {
+        L.wbase[w] = b;
+        b += L.wrows[w];
+      }
+    }
 #ifndef W2_NO_C
     W2_STAMPW(wi, 8, -1);
-    wsync();   // vout
-    // C5: key lane: carried rows, survivors, state commit
-    if (klane && kc > 0) {
-      const int64_t kl = ((int64_t)tid << lg) | bucket;
-      const int64_t kv = kl * p.key_stride + p.key_offset;
-      if (cm) {
-        const int64_t bts = ts_base + (int64_t)L.rts[fbs];
-        const uint64_t b0 = NW > 0 ? L.rcap[0][fbs] : 0ull, b1 = NW > 1 ? L.rcap[NW > 1 ? 1 : 0][fbs] : 0ull;
-        const unsigned long long rb = obase + L.vout[r0];
-        const int64_t bseq = seq_base + (int64_t)L.rseq[fbs];
-#ifndef W2_NO_EMIT
-        w2_emit<KR>(a, rb, kv, e00, e01, b0, b1, bts, bseq);
-        if (cm > 1) w2_emit<KR>(a, rb + 1, kv, e10, e11, b0, b1, bts, bseq);
-        for (int j = 2; j < cm; ++j)   // long lists: slots in HBM (rare)
-          w2_emit<KR>(a, rb + j, kv, c1 ? slot_word(cfirst + j, 2) : 0ull, c2 ? slot_word(cfirst + j, 3) : 0ull, b0,
-                      b1, bts, bseq);
-#endif
-      }
+    // C5: key lane: survivors and state commit (no output yet: the carried
+    // rows are emitted after the reservation, from values read before it)
+    int nn_new = n;
+    uint32_t ovo_new = ovo;
+    // a lane whose carried rows read slots >= 2 from HBM (no scratch copy)
+    // commits only after emitting them: the commit rewrites those slots
+    const bool late = klane && kc > 0 && cm > 2 && scb < 0;
+    auto commit = [&]() {
       const bool prune = W >= 0 && hasa;
       const int64_t last_a_ts = ts_base + (int64_t)last_a;
       int nn = 0;
@@ -703,11 +743,14 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
                  cp1 < 0 ? (uint64_t)ats : (cp1 == 0 ? a0 : a1));
       }
       dirty |= nn != n;
-      if (nn > S) ovo = noff | kOvoWr;
-      n = nn;
-    }
-    W2_STAMPW(wi, 9, -1);
+      nn_new = nn;
+      if (nn > S) ovo_new = noff | kOvoWr;
+    };
+    if (klane && kc > 0 && !late) commit();
 #endif
+    lds_barrier();   // #D: the output bases
+    const unsigned long long obase = L.wbase[wave];
+    W2_STAMPW(wi, 9, -1);
     // ================= C0: the next window's records go out only now: from
     // here on this wave issues stores only, so nothing waits for these loads
     // until the next window's phase A (vmcnt counts loads and stores in issue
@@ -726,6 +769,25 @@ __global__ __launch_bounds__(kCfWalkThreads, W2_MINW) void k_cfwalk2(CfWalkArgs 
       }
     }
 #ifndef W2_NO_C
+    // C5b: key lane: carried rows completed by the run's first B (captures
+    // read before the commit; slots >= 2 from this window's scratch copy)
+    if (klane && kc > 0 && cm) {
+      const int64_t kv = (((int64_t)tid << lg) | bucket) * p.key_stride + p.key_offset;
+      const int64_t bts = ts_base + (int64_t)L.rts[fbs];
+      const uint64_t b0 = NW > 0 ? L.rcap[0][fbs] : 0ull, b1 = NW > 1 ? L.rcap[NW > 1 ? 1 : 0][fbs] : 0ull;
+      const unsigned long long rb = obase + L.vout[r0];
+      const int64_t bseq = seq_base + (int64_t)L.rseq[fbs];
+#ifndef W2_NO_EMIT
+      w2_emit<KR>(a, rb, kv, e00, e01, b0, b1, bts, bseq);
+      if (cm > 1) w2_emit<KR>(a, rb + 1, kv, e10, e11, b0, b1, bts, bseq);
+      for (int j = 2; j < cm; ++j)   // long lists (rare)
+        w2_emit<KR>(a, rb + j, kv, c1 ? slot_word(cfirst + j, 2) : 0ull, c2 ? slot_word(cfirst + j, 3) : 0ull, b0, b1,
+                    bts, bseq);
+#endif
+    }
+    if (late) commit();
+    n = nn_new;
+    ovo = ovo_new;
     // C6: record matches, lane per sorted position (stores only)
     for (uint32_t e0 = 0; e0 < nl; e0 += 64) {
       const uint32_t e = e0 + lane;
