@@ -71,6 +71,9 @@ def parse():
                     help="key buckets = 2^n (0: engine default, <= 512 keys per bucket)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity check")
+    ap.add_argument("--exchange", choices=["padded", "twophase"], default="padded",
+                    help="key shuffle of pattern records: fixed owner segments with in-band counts (no host "
+                         "round trip per step) or counts first, then an exact alltoallv")
     ap.add_argument("--ingest", choices=["shuffle", "prepartitioned", "host", "host-pageable"],
                     default="shuffle",
                     help="multi-GPU pattern input: engine key shuffle over RCCL, or keyed upstream; "
@@ -461,12 +464,52 @@ def main():
         bufs[("send", j)] = recs
         return recs, counts
 
+    seg_cap = [0]
+
+    def run_padded(blist):
+        # Padded exchange (keyed pattern records): fixed owner segments with
+        # in-band counts, one equal-split all-to-all, nothing read back — the
+        # step loop has no host round trip.  route_padded(wait=True) orders
+        # the route of step s+1 after torch's stream, i.e. after the
+        # all-to-all that last read its send buffer; the walk of step s keeps
+        # running on the engine stream.
+        from flink_siddhi import shuffle
+        cap = seg_cap[0]
+        for i, d in enumerate(blist):
+            j = i % 2
+            segs = rt.route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
+                                   seq0=d["first"], seg_cap=cap, streams=d["stream"],
+                                   out=bufs.get(("psend", j)))
+            bufs[("psend", j)] = segs
+            torch.cuda.current_stream().wait_stream(guard[j])   # the walk that last read precv[j]
+            recv = shuffle.exchange_padded(segs, world, out=bufs.get(("precv", j)))
+            bufs[("precv", j)] = recv
+            rt.send_padded(recv, world, cap, n, signal=False)
+            rt.signal(guard[j])
+        rt.flush()
+
     def run_shuffle(blist):
         # Software pipeline over steps, double-buffered send / receive: the
         # route of step s+1 (engine route stream) and the record all-to-all of
         # step s+1 (RCCL) run while the walk of step s runs on the engine stream.
         from flink_siddhi import shuffle
         if not blist:
+            return
+        if pattern and args.exchange == "padded" and seg_cap[0] == 0:
+            # calibrate the segment capacity on the first warm-up step
+            # (two-phase: host counts), then every later step is padded
+            recs, counts = route(blist[0], 0)
+            seg_cap[0] = shuffle.calibrated_capacity(counts)
+            recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get(("recv", 0)))
+            bufs[("recv", 0)] = recv
+            send_fn(recv, m, n, signal=False)
+            rt.signal(guard[0])
+            blist = blist[1:]
+            if not blist:
+                rt.flush()
+                return
+        if pattern and args.exchange == "padded":
+            run_padded(blist)
             return
         cur = route(blist[0], 0)
         for i in range(len(blist)):
@@ -602,8 +645,11 @@ def main():
                         "keys": args.keys, "keys_dist": args.keys_dist if args.keys_dist == "uniform" else "zipf(s=1.1)",
                         "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
                         "chunk_events": args.chunk, "parallelism": "key-sharded x%d" % world,
-                        "ingest": (("%s all-to-all key shuffle" % ("rccl" if _coll_device() == "cuda"
-                                                                    else "gloo host-staged"))
+                        "ingest": (("%s all-to-all key shuffle (%s)" % ("rccl" if _coll_device() == "cuda"
+                                                                         else "gloo host-staged",
+                                                                         "padded segments, in-band counts"
+                                                                         if args.exchange == "padded"
+                                                                         else "two-phase"))
                                     if shuffle_mode else
                                    "pre-partitioned (keyed upstream)") if world > 1 else
                                   ("host (%s memory over PCIe)" % ("pinned" if args.ingest == "host" else "pageable")

@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
 #pragma unroll 1
     for (int i = 0; i < PER; ++i) {
       const uint32_t q = tid + i * NT;
-      if (q >= nw) continue;
+      if (q >= nw || (a.ablate & 4)) continue;   // ablate 4 (diagnostics): no record-match stores
       const uint32_t kr = L.skr[q];
       const uint16_t nb = L.nextb[q];
       if (!((kr >> 12) & ROLE_A) || nb == kNoB) continue;

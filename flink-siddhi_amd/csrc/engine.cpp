@@ -1774,6 +1774,10 @@ int error_status(cep_app* a, unsigned int e) {
     return fail(a, CEP_E_CAPACITY, "more distinct partition values than key_capacity (sparse_keys)");
   if (e & ERR_KEY_RANGE)
     return fail(a, CEP_E_CAPACITY, "partition key outside [0, key_capacity) or not owned by this shard");
+  if (e & ERR_SHUFFLE_CAP)
+    return fail(a, CEP_E_CAPACITY,
+                "padded key shuffle: an owner segment overflowed seg_cap (its excess records were dropped; "
+                "raise seg_cap or use the two-phase exchange)");
   if (e & ERR_TS_SPAN)
     return fail(a, CEP_E_ARG, "timestamps of one chunk lie more than 2^31 ms apart (lower chunk_events)");
   if (e & ERR_OUT_CAP) return fail(a, CEP_E_DEVICE, "output capacity exceeded");
@@ -2515,6 +2519,14 @@ int cep_stream_signal(cep_app* a, void* hip_stream) {
   return CEP_OK;
 }
 
+int cep_route_signal(cep_app* a, void* hip_stream) {
+  if (!a) return CEP_E_ARG;
+  if (hipEventRecord(a->r_ready, a->rstream) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)hip_stream, a->r_ready, 0) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "cep_route_signal: invalid stream");
+  return CEP_OK;
+}
+
 int cep_set_enabled(cep_app* a, int enabled) {
   if (!a) return CEP_E_ARG;
   a->enabled = enabled != 0;
@@ -2932,9 +2944,12 @@ int cep_record_words(cep_app* a) {
   return a->pats[0].pa.rec_words + 1;   // wide record: [hdr, seq, ts, carried...]
 }
 
-int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out,
-                    int64_t rec_cap, int64_t* counts_host) {
-  if (!a || !b || !counts_host || world <= 0) return CEP_E_ARG;
+// seg_cap == 0: owner-contiguous output, counts read back (cep_route_batch);
+// seg_cap > 0: padded owner segments with in-band counts, nothing read back
+// (cep_route_batch_padded).
+static int route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out,
+                       int64_t rec_cap, int64_t* counts_host, int64_t seg_cap) {
+  if (!a || !b || world <= 0 || (seg_cap == 0 && !counts_host) || seg_cap < 0) return CEP_E_ARG;
   if (world > kMaxWorld) return fail(a, CEP_E_ARG, "world exceeds " + std::to_string(kMaxWorld));
   if (a->pats.size() != 1 || a->app.queries.size() != 1)
     return fail(a, CEP_E_UNSUPPORTED, "key shuffle needs an app with exactly one keyed pattern");
@@ -2942,12 +2957,20 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   const Query& q = a->app.queries[rt.q];
   if (q.key_col_a < 0 || q.key_col_b < 0)
     return fail(a, CEP_E_UNSUPPORTED, "key shuffle needs a partitioned pattern");
-  for (int d = 0; d < world; ++d) counts_host[d] = 0;
-  if (b->n == 0) return CEP_OK;
-  // the gather writes rec_out as soon as it runs: at most n records are
-  // routed, so a buffer of n records can never overrun (checked up front)
-  if (!rec_out || rec_cap < b->n)
-    return fail(a, CEP_E_ARG, "rec_out must hold at least n records (" + std::to_string(b->n) + ")");
+  if (seg_cap == 0) {
+    for (int d = 0; d < world; ++d) counts_host[d] = 0;
+    if (b->n == 0) return CEP_OK;
+    // the gather writes rec_out as soon as it runs: at most n records are
+    // routed, so a buffer of n records can never overrun (checked up front)
+    if (!rec_out || rec_cap < b->n)
+      return fail(a, CEP_E_ARG, "rec_out must hold at least n records (" + std::to_string(b->n) + ")");
+  } else {
+    // every rank ships world segments each step, so the null records need a
+    // ts / seq of this batch (its first and last rows)
+    if (b->n == 0) return fail(a, CEP_E_ARG, "padded key shuffle needs a non-empty batch");
+    if (!rec_out || rec_cap < (int64_t)world * (1 + seg_cap))
+      return fail(a, CEP_E_ARG, "rec_out must hold world * (1 + seg_cap) records");
+  }
   RowsArgs rows{};
   int slot;
   bool direct;
@@ -2981,6 +3004,7 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   ra.arena = (uint64_t*)a->route_arena.p;
   ra.tcount = (uint32_t*)a->route_tcount.p;
   ra.err = (unsigned int*)a->rerr.p;
+  ra.seg_cap = seg_cap;
   {
     LaunchTimer t(a, CEP_K_ROUTE, rs);
     if (fast) {
@@ -2998,8 +3022,16 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
       launch_route(ra, ntiles, rt.part_vm, (uint32_t*)a->route_toffs.p,
                    (unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, rs);
     }
+    if (seg_cap > 0) launch_route_pad(ra, (const unsigned long long*)a->route_dcount.p, (uint64_t*)rec_out, rs);
   }
   if (slot >= 0) hipEventRecord(a->hs[slot].free, rs);
+  if (seg_cap > 0) {
+    // the route's error bits travel in the segment headers (every owner
+    // reports them at its next flush); cleared behind the pad kernel
+    hipMemsetAsync(a->rerr.p, 0, 64, rs);
+    a->batches++;
+    return hipGetLastError() == hipSuccess ? CEP_OK : fail(a, CEP_E_DEVICE, "padded route launch failed");
+  }
   // the per-owner counts: W words, read back on the route stream only (the
   // all-to-all's split sizes are host values); the engine stream keeps going
   std::vector<unsigned long long> dc(world);
@@ -3022,6 +3054,17 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   }
   a->batches++;
   return CEP_OK;
+}
+
+int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out,
+                    int64_t rec_cap, int64_t* counts_host) {
+  return route_batch(a, b, world, seq0, rec_out, rec_cap, counts_host, 0);
+}
+
+int cep_route_batch_padded(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* seg_out,
+                           int64_t seg_out_cap, int64_t seg_cap) {
+  if (seg_cap <= 0) return CEP_E_ARG;
+  return route_batch(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap);
 }
 
 // Row shuffle plan: per input handle the owner key column (-1: any owner,
@@ -3096,6 +3139,27 @@ int cep_send_records(cep_app* a, const void* recs, int64_t n, int64_t events_rep
   rows.input = rt.pa.a_stream;
   a->batches++;
   return run_pattern(a, rt, rows, (const uint64_t*)recs, rt.pa.rec_words + 1);
+}
+
+int cep_send_records_padded(cep_app* a, const void* segs, int world, int64_t seg_cap,
+                            int64_t events_represented) {
+  if (!a || !segs || world <= 0 || world > kMaxWorld || seg_cap <= 0) return CEP_E_ARG;
+  if (!a->enabled) return CEP_OK;
+  if (a->pats.size() != 1 || a->app.queries.size() != 1)
+    return fail(a, CEP_E_UNSUPPORTED, "records need an app with exactly one keyed pattern");
+  a->events_in += events_represented;
+  PatternRT& rt = a->pats[0];
+  const int wrw = rt.pa.rec_words + 1;
+  // the headers' counts / error bits -> this engine's error word (reported
+  // by the next flush); the null records flow through the partitions, which
+  // skip role-0 records, so no count is read back here
+  launch_route_check((const uint64_t*)segs, world, seg_cap, wrw, (unsigned int*)a->err.p, a->stream);
+  RowsArgs rows{};
+  rows.n = (int64_t)world * (1 + seg_cap);
+  rows.row0 = 0;
+  rows.input = rt.pa.a_stream;
+  a->batches++;
+  return run_pattern(a, rt, rows, (const uint64_t*)segs, wrw);
 }
 
 int cep_row_words(cep_app* a) {

@@ -63,6 +63,7 @@ enum : uint32_t {
   ERR_POOL = 32u,            // pending overflow pool exhausted
   ERR_KEYMAP = 64u,          // more distinct partition values than key_capacity (sparse keys)
   ERR_TS_SPAN = 128u,        // a chunk's ts lie more than 2^31 ms either side of its first row
+  ERR_SHUFFLE_CAP = 256u,    // padded key shuffle: an owner segment held more than seg_cap records
 };
 
 // Per-key state header: pending count (bits 0-7, <= S) | started << 8 |
@@ -201,6 +202,9 @@ struct RouteArgs {
   uint64_t* arena;             // [ntiles][tile_rows * wrw], owner-grouped per tile
   uint32_t* tcount;            // [ntiles][world] kept rows per owner
   unsigned int* err;
+  // > 0: padded segments (cep_route_batch_padded): owner d's records go to
+  // out + (d * (1 + seg_cap) + 1) * wrw, at most seg_cap of them
+  int64_t seg_cap;
 };
 
 struct WalkArgs {
@@ -550,6 +554,10 @@ void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
                   unsigned long long* dcount, uint64_t* out, hipStream_t s);
 void launch_route_collect(const RouteArgs& a, int64_t ntiles, uint32_t* toffs,
                           unsigned long long* dcount, uint64_t* out, hipStream_t s);
+// padded key shuffle: segment headers + null tails (sender), header check (owner)
+void launch_route_pad(const RouteArgs& a, const unsigned long long* dcount, uint64_t* out, hipStream_t s);
+void launch_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, unsigned int* err,
+                        hipStream_t s);
 void launch_route_rows(const RowRouteArgs& a, int64_t ntiles, uint32_t* toffs,
                        unsigned long long* dcount, uint64_t* out, hipStream_t s);
 void launch_unpack_rows(const RowUnpackArgs& a, hipStream_t s);

@@ -902,11 +902,76 @@ __global__ __launch_bounds__(256) void k_route_gather(RouteArgs a, int64_t ntile
   for (int d = 0; d < a.world; ++d) {
     const uint32_t c = a.tcount[t * a.world + d];
     const uint64_t* s = a.arena + (t * (int64_t)a.tile_rows + src) * wrw;
-    uint64_t* o = out + (int64_t)(obase + toffs[(int64_t)d * ntiles + t]) * wrw;
-    for (int64_t w = threadIdx.x; w < (int64_t)c * wrw; w += blockDim.x) o[w] = s[w];
+    const uint32_t to = toffs[(int64_t)d * ntiles + t];
+    int64_t n = c;
+    uint64_t* o;
+    if (a.seg_cap > 0) {   // padded: owner d's segment, records past seg_cap dropped (flagged by k_route_pad)
+      n = (int64_t)to >= a.seg_cap ? 0 : (c < a.seg_cap - (int64_t)to ? (int64_t)c : a.seg_cap - (int64_t)to);
+      o = out + ((int64_t)d * (1 + a.seg_cap) + 1 + to) * wrw;
+    } else {
+      o = out + (int64_t)(obase + to) * wrw;
+    }
+    for (int64_t w = threadIdx.x; w < n * wrw; w += blockDim.x) o[w] = s[w];
     src += c;
     obase += dcount[d];
   }
+}
+
+// Padded key shuffle, sender side: owner d's segment is one header record
+// then seg_cap record slots.  The header and the unused slots are null
+// records (role 0: every partition skips them) whose ts / seq keep the
+// receiver's concatenation in event-time order: the header carries the
+// batch's first row, the tail its last (rank r's batch precedes rank r + 1's).
+// Header word 0 = the owner's true record count (low 32 bits) | route error
+// bits << 40 | 1 << 63 when the count exceeds seg_cap; owners check it
+// (k_route_check) without a host round trip.
+__global__ __launch_bounds__(256) void k_route_pad(RouteArgs a, const unsigned long long* dcount, uint64_t* out) {
+  const int d = blockIdx.y;
+  const int wrw = a.wrw;
+  const unsigned long long cnt = dcount[d];
+  const int64_t used = (int64_t)cnt < a.seg_cap ? (int64_t)cnt : a.seg_cap;
+  const int64_t r0 = a.rows.row0, r1 = a.rows.row0 + a.rows.n - 1;
+  uint64_t* seg = out + (int64_t)d * (1 + a.seg_cap) * wrw;
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)wrw) {
+    const unsigned int e = *(volatile unsigned int*)a.err;
+    uint64_t h = 0;
+    if (threadIdx.x == 0)
+      h = (cnt & 0xffffffffull) | ((uint64_t)(e & 0xffffu) << 40) | ((int64_t)cnt > a.seg_cap ? 1ull << 63 : 0ull);
+    else if (threadIdx.x == 1)
+      h = (uint64_t)a.seq0;
+    else if (threadIdx.x == 2)
+      h = (uint64_t)a.rows.ts[r0];
+    seg[threadIdx.x] = h;
+  }
+  const uint64_t tseq = (uint64_t)(a.seq0 + a.rows.n - 1), tts = (uint64_t)a.rows.ts[r1];
+  const int64_t nul = (a.seg_cap - used) * wrw;
+  uint64_t* tail = seg + (1 + used) * wrw;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nul; w += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(w % wrw);
+    tail[w] = f == 1 ? tseq : (f == 2 ? tts : 0ull);
+  }
+}
+
+// Owner side: a flagged header (overflowed segment or a sender-side route
+// error) becomes the owner's error word, reported by its next flush.
+__global__ void k_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, unsigned int* err) {
+  const int d = threadIdx.x;
+  if (d >= world) return;
+  const uint64_t h = segs[(int64_t)d * (1 + seg_cap) * wrw];
+  unsigned int e = (unsigned int)((h >> 40) & 0xffffu);
+  if (h >> 63) e |= ERR_SHUFFLE_CAP;
+  if (e) atomicOr(err, e);
+}
+
+void launch_route_pad(const RouteArgs& a, const unsigned long long* dcount, uint64_t* out, hipStream_t s) {
+  const int64_t per = (a.seg_cap * a.wrw + 255) / 256;
+  const unsigned bx = (unsigned)(per < 1 ? 1 : (per > 1024 ? 1024 : per));
+  hipLaunchKernelGGL(k_route_pad, dim3(bx, (unsigned)a.world), dim3(256), 0, s, a, dcount, out);
+}
+
+void launch_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, unsigned int* err,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_route_check, dim3(1), dim3(64), 0, s, segs, world, seg_cap, wrw, err);
 }
 
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

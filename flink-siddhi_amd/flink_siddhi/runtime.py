@@ -292,6 +292,55 @@ class SiddhiAppRuntime:
                                               C.c_void_p(out.data_ptr()), out.shape[0], counts))
         return out, [int(c) for c in counts]
 
+    def route_padded(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int, seg_cap: int,
+                     streams=None, out=None, wait: bool = True):
+        """Padded sender side (cep_route_batch_padded): a uint64 device tensor
+        [world * (1 + seg_cap), record_words] of fixed owner segments with the
+        counts in-band (segment headers).  Nothing is read back: the route is
+        only queued, so the step needs no host round trip."""
+        import torch
+        h = self.input_handle(stream_id)
+        defs = self.stream_definition(stream_id)
+        if not _is_device(ts):
+            raise ValueError("route_padded() takes device-resident columns")
+        keep = []
+        ptrs = (C.c_void_p * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            p, k = _ptr(c, np.dtype(L.NUMPY_DTYPES[defs[i][1]]), True)
+            ptrs[i] = p
+            keep.append(k)
+        sp = None
+        if streams is not None:
+            sp, k = _ptr(streams, np.dtype("uint8"), True)
+            keep.append(k)
+        rows = world * (1 + int(seg_cap))
+        w = self.record_words()
+        if out is None or out.shape[0] < rows or out.shape[1] != w:
+            out = torch.empty((rows, w), dtype=torch.int64, device=ts.device)
+        b = L.cep_batch(n=_len(ts), ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
+                        cols=ptrs, on_device=1)
+        if wait:
+            self._wait_producer(ts)
+        self._check(self._lib.cep_route_batch_padded(self._h, C.byref(b), world, seq0,
+                                                     C.c_void_p(out.data_ptr()), out.shape[0], int(seg_cap)))
+        # torch's stream (the all-to-all) must not read the segments before the
+        # route stream wrote them; the walk queued on the engine stream is not
+        # waited for
+        s = torch.cuda.current_stream(ts.device).cuda_stream
+        self._check(self._lib.cep_route_signal(self._h, C.c_void_p(s)))
+        return out[:rows]
+
+    def send_padded(self, segs, world: int, seg_cap: int, events_represented: int = 0,
+                    signal: bool = True):
+        """Owner side of the padded shuffle: the world received segments in
+        source-rank order.  An overflowed segment fails the next flush."""
+        if getattr(segs, "is_cuda", False):
+            self._wait_producer(segs)
+        self._check(self._lib.cep_send_records_padded(self._h, C.c_void_p(segs.data_ptr()), world,
+                                                      int(seg_cap), events_represented))
+        if signal and getattr(segs, "is_cuda", False):
+            self._signal_consumer(segs)
+
     def partition_channels(self, stream_id: str, ts, cols: Sequence, key_field: Optional[str],
                            nchan: int, seq0: int = 0, keys: bool = False):
         """Dynamic-path routing of a device batch (AddRouteOperator.java:83-92 ->

@@ -92,3 +92,44 @@ def exchange(records: torch.Tensor, counts: Sequence[int], out: torch.Tensor = N
         dist.all_to_all_single(out[:m].view(-1), records[:n].reshape(-1),
                                output_split_sizes=osz, input_split_sizes=isz)
     return out, m, recv_counts
+
+
+def padded_capacity(n: int, world: int, slack: float = 0.25, floor: int = 1024) -> int:
+    """Records per owner segment for the padded exchange: the even share of
+    a rank's n rows plus `slack` of it (owners are key % world, so for keys
+    spread over many values the counts sit close to n / world) and a floor
+    for small batches.  The caller may pass any larger value; an overflow is
+    reported by the owner's next flush (cep_send_records_padded)."""
+    share = -(-int(n) // int(world))
+    return int(share + share * slack) + floor
+
+
+def exchange_padded(segs: torch.Tensor, world: int, out: torch.Tensor = None) -> torch.Tensor:
+    """Equal-split all-to-all of `world` fixed owner segments (rows [d * S,
+    (d + 1) * S) go to rank d): no split sizes, so no count exchange and no
+    host round trip.  Returns the world received segments in source-rank
+    order (the layout cep_send_records_padded reads)."""
+    if out is None or out.shape != segs.shape:
+        out = torch.empty_like(segs)
+    if _host_staged() and segs.is_cuda:
+        host_out = torch.empty(segs.numel(), dtype=segs.dtype)
+        dist.all_to_all_single(host_out, segs.reshape(-1).cpu())
+        out.view(-1).copy_(host_out)
+    else:
+        dist.all_to_all_single(out.view(-1), segs.reshape(-1))
+    return out
+
+
+def calibrated_capacity(counts: Sequence[int], slack: float = 0.15, floor: int = 1024) -> int:
+    """Segment capacity from one measured step (a two-phase route's host
+    counts, e.g. during warm-up): the largest per-owner count over all ranks
+    plus `slack` of it.  One host all-reduce, outside the step loop."""
+    m = torch.tensor([max(counts) if len(counts) else 0], dtype=torch.int64)
+    g = _count_group()
+    if g == "device":
+        m = m.cuda()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    else:
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=g)
+    top = int(m.item())
+    return int(top + top * slack) + floor

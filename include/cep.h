@@ -283,6 +283,32 @@ int cep_route_batch(cep_app* app, const cep_batch* batch, int world,
                     int64_t* counts_host);
 int cep_send_records(cep_app* app, const void* recs, int64_t n,
                      int64_t events_represented);
+/* Padded key shuffle: the step without a host round trip.  Like
+ * cep_route_batch, but shard r's records land in a fixed segment of
+ * 1 + seg_cap records at seg_out[r * (1 + seg_cap)]: one header record (word
+ * 0 = the shard's record count | route error bits << 40 | 1 << 63 when the
+ * count exceeds seg_cap; words 1 / 2 = seq / ts of the batch's first row),
+ * then the records, then null records (role 0, seq / ts of the batch's last
+ * row) up to seg_cap.  Nothing is read back: the call returns once the route
+ * is queued on the engine's route stream.  The caller moves the segments with
+ * one equal-split all-to-all (no host split sizes) and feeds the world
+ * received segments, in source-rank order, to cep_send_records_padded, which
+ * checks the headers on the device: a segment that overflowed seg_cap (its
+ * excess records dropped) or carries a sender's route error makes the next
+ * cep_flush / cep_watermark fail (CEP_E_CAPACITY / the route error).  That
+ * step's output is then incomplete: like a failed Flink task, the caller
+ * restores the last snapshot (cep_restore) and replays from it with the
+ * two-phase exchange above or a larger seg_cap.  Needs a
+ * non-empty batch (n > 0).  Replaces the same keyBy shuffle as
+ * cep_route_batch (router/HashPartitioner.java:24-26). */
+int cep_route_batch_padded(cep_app* app, const cep_batch* batch, int world,
+                           int64_t seq0, void* seg_out, int64_t seg_out_cap,
+                           int64_t seg_cap);
+int cep_send_records_padded(cep_app* app, const void* segs, int world,
+                            int64_t seg_cap, int64_t events_represented);
+/* Make hip_stream wait for the routes queued so far (the route stream only:
+ * the all-to-all of step s+1 need not wait for the walk of step s). */
+int cep_route_signal(cep_app* app, void* hip_stream);
 /* Row shuffle for apps with several queries (sequences, aggregations, more
  * than one pattern; BASELINE config 5 across GPUs).  No predicate push-down:
  * a sequence needs every row of its streams (strict contiguity).  Every row

@@ -150,3 +150,90 @@ def test_pipelined_route_overlaps_walk(world):
     assert_same_rows(got, want, "pipelined world=%d" % world)
     for rt in rts:
         rt.shutdown()
+
+
+def _padded_round(world, n_per, keys, seg_cap, steps=1, cap_fn=None):
+    """Sources route with cep_route_batch_padded; owner r receives segment r
+    of every source in source order (the equal-split all-to-all) and feeds
+    them to cep_send_records_padded.  No counts are read back anywhere."""
+    plan = workload.PATTERN_PLAN
+    senders = [fs.SiddhiAppRuntime(plan) for _ in range(world)]
+    owners = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=8192)
+              for r in range(world)]
+    for o in owners:
+        o.add_callback("O")
+    for s in range(steps):
+        sent = []
+        for src in range(world):
+            g = s * world + src
+            w = workload.generate(g * n_per, n_per, keys, rate=1)
+            d = _dev(w)
+            segs = senders[src].route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
+                                             world, seq0=g * n_per, seg_cap=seg_cap, streams=d["stream"])
+            sent.append(segs)
+        torch.cuda.synchronize()
+        S = 1 + seg_cap
+        for r in range(world):
+            recv = torch.cat([sent[src][r * S:(r + 1) * S] for src in range(world)], dim=0)
+            owners[r].send_padded(recv, world, seg_cap, n_per)
+    return senders, owners
+
+
+@pytest.mark.parametrize("path", ["cf", "general"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_padded_exchange_matches_oracle(world, path, monkeypatch):
+    # VERDICT r03 item 6: fixed per-peer segments with in-band counts; the
+    # null records (header + tail) must be invisible to both partitions
+    if path == "general":
+        monkeypatch.setenv("CEP_NO_CF", "1")
+    else:
+        monkeypatch.delenv("CEP_NO_CF", raising=False)
+    from flink_siddhi import shuffle
+    n_per, keys, steps = 12000, 600, 2
+    cap = shuffle.padded_capacity(n_per, world)
+    senders, owners = _padded_round(world, n_per, keys, cap, steps=steps)
+    got = []
+    for o in owners:
+        o.flush()
+        got += engine_rows(o.collect("O"))
+    got.sort(key=lambda t: t[1])
+    w = workload.generate(0, steps * world * n_per, keys, rate=1)
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(w)).get("O", [])
+    assert len(want) > 100
+    assert_same_rows(got, want, "padded shuffle world=%d" % world)
+    for rt in owners + senders:
+        rt.shutdown()
+
+
+def test_padded_segment_headers_carry_the_counts():
+    world, n, keys = 4, 30000, 900
+    w = workload.generate(0, n, keys, rate=1)
+    d = _dev(w)
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world, seq0=5,
+                            streams=d["stream"])
+    recs = recs[:sum(counts)].cpu().numpy().copy()
+    cap = max(counts) + 3
+    segs = rt.route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world, seq0=5,
+                           seg_cap=cap, streams=d["stream"])
+    torch.cuda.synchronize()
+    s = segs.cpu().numpy().reshape(world, 1 + cap, -1)
+    off = np.concatenate([[0], np.cumsum(counts)])
+    for r in range(world):
+        h = s[r, 0]
+        assert int(h[0]) & 0xffffffff == counts[r] and (int(h[0]) >> 32) & 0xff == 0
+        assert int(h[1]) == 5 and int(h[2]) == int(w["ts"][0])
+        assert (s[r, 1:1 + counts[r]] == recs[off[r]:off[r + 1]]).all()
+        tail = s[r, 1 + counts[r]:]
+        assert ((tail[:, 0] >> 32) & 0xff == 0).all()          # role 0: null records
+        assert (tail[:, 1] == 5 + n - 1).all() and (tail[:, 2] == int(w["ts"][-1])).all()
+    rt.shutdown()
+
+
+def test_padded_overflow_fails_the_next_flush():
+    world, n_per, keys = 2, 12000, 600
+    senders, owners = _padded_round(world, n_per, keys, seg_cap=64)
+    with pytest.raises(fs.CepCapacityError, match="seg_cap"):
+        owners[0].flush()
+    for rt in owners + senders:
+        rt.shutdown()

@@ -33,7 +33,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, q, side=False):
+def _rank_main(rank, world, port, q, side=False, padded=False):
     if side:   # counts over a separate gloo group, as beside RCCL on GPUs
         os.environ["CEP_COUNT_GROUP"] = "side"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -53,9 +53,22 @@ def _rank_main(rank, world, port, q, side=False):
             rows.append(np.stack([seq[sel], w["k"][sel].astype(np.int64), w["ts"][sel],
                                   w["id"][sel].astype(np.int64), w["price"][sel].view(np.int64),
                                   w["stream"][sel].astype(np.int64)], axis=1))
-        recs = torch.from_numpy(np.concatenate(rows, axis=0).copy())
-        got, m, src_counts = shuffle.exchange(recs, counts)
-        r = got[:m].numpy()
+        if padded:
+            # cep_route_batch_padded's layout: per owner one header row (the
+            # count in-band), the rows, null rows up to cap; equal-split
+            # all-to-all, no count exchange (the step has no host round trip)
+            cap = shuffle.padded_capacity(N_PER_RANK, world, floor=16)
+            segs = np.zeros((world, 1 + cap, 6), dtype=np.int64)
+            for d in range(world):
+                segs[d, 0, 0] = counts[d]
+                segs[d, 1:1 + counts[d]] = rows[d]
+            got = shuffle.exchange_padded(torch.from_numpy(segs.reshape(world * (1 + cap), 6)), world)
+            g = got.numpy().reshape(world, 1 + cap, 6)
+            r = np.concatenate([g[s, 1:1 + int(g[s, 0, 0])] for s in range(world)], axis=0)
+        else:
+            recs = torch.from_numpy(np.concatenate(rows, axis=0).copy())
+            got, m, src_counts = shuffle.exchange(recs, counts)
+            r = got[:m].numpy()
         assert (np.diff(r[:, 0]) > 0).all(), "received records not in global arrival order"
         assert (r[:, 1] % world == rank).all(), "received a key this rank does not own"
         ev = {"k": r[:, 1].astype(np.int32), "ts": r[:, 2], "id": r[:, 3].astype(np.int32),
@@ -71,13 +84,13 @@ def _rank_main(rank, world, port, q, side=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("side", [False, True])
-def test_key_shuffle_gloo_world2_matches_single_process(side):
-    world = 2
+@pytest.mark.parametrize("side,padded,world", [(False, False, 2), (True, False, 2), (False, True, 2),
+                                               (False, True, 3)])
+def test_key_shuffle_gloo_matches_single_process(side, padded, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, side)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, side, padded)) for r in range(world)]
     for p in procs:
         p.start()
     allout = q.get(timeout=240)
