@@ -79,8 +79,11 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 }  // namespace
 
 // ============================================================== k_cfpart ==
+#ifndef CF_PART_MINW   // waves per SIMD the register budget is set for
+#define CF_PART_MINW (kCfPartThreads == 512 ? 4 : 1)
+#endif
 template <int NW, bool FR, int NP = kPref>   // FR: rows are received shuffle records; NP prefetched columns
-__global__ __launch_bounds__(kCfPartThreads, kCfPartThreads == 512 ? 4 : 1) void k_cfpart(CfPartArgs a) {
+__global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
   __shared__ uint32_t scratch[NT / 64 + 1];
@@ -765,6 +768,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       L.khasa[tid] = 0;
     }
     lds_barrier();
+    if (wi == 1) CF_STAMP(9);   // window 1: the window's record table is built
     // ---- every record of the window in flight at once (one pass over the
     // scattered segments: the records stay in registers through the sort);
     // key counts
@@ -1128,6 +1132,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     // the previous window used, read by nobody since: zeroed without a
     // second barrier (its counts are added after the next window's first)
     lds_barrier();
+    CF_STAMP(8);   // window 1 only: after the window-end barrier
     kbuf ^= 1;
     for (int k = tid; k <= kpb; k += NT) L.kstart[kbuf][k] = 0;
   }

@@ -234,6 +234,20 @@ __device__ __forceinline__ void cf_load_cols(const RowsArgs& rows, const PrefPla
     }
 }
 
+// Inclusive scan over the 64 lanes with DPP row shifts and row broadcasts
+// (VALU-only: no LDS round trip per step, unlike __shfl_up).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  // within each row of 16 lanes: shifts 1, 2, 4, 8 (lanes without a source add 0)
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  // across rows: lane 15 into rows 1 and 3, then lane 31 into rows 2 and 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return x;
+}
+
 // XCD-aware bucket order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
 // §Workgroup dispatch), so consecutive buckets — which share tile-offset
 // cache lines — are given to blocks of one XCD.  Speed only, never correctness.

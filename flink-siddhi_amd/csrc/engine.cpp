@@ -1093,6 +1093,19 @@ int create_runtime(cep_app* a) {
     }
     // group-by and N-state / sequence walks live in the VM build of k_walk
     rt.walk_vm = walk_vm;
+    // N-state patterns / sequences: partial lists longer than pending_slots
+    // continue in the pending pool (nfa_key), as on the closed-form path
+    if (q.nfa) {
+      const int plg = a->opt.pending_pool_log2 > 0 ? std::min(a->opt.pending_pool_log2, 30) : 20;
+      rt.pool_cap = (int64_t)1 << plg;
+      const bool ok = dev_ensure(&rt.kext, (size_t)rt.kstride * 8, a->stream, false) &&
+                      dev_ensure(&rt.pool[0], (size_t)rt.pool_cap * p.slot_words * 8, a->stream, false) &&
+                      dev_ensure(&rt.pool[1], (size_t)rt.pool_cap * p.slot_words * 8, a->stream, false) &&
+                      dev_ensure(&rt.pool_cur, 64, a->stream, false);
+      if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (pending pool)");
+      hipMemset(rt.kext.p, 0, (size_t)rt.kstride * 8);
+      rt.extra_bound += rt.pool_cap;   // pool partials may complete too
+    }
     // closed-form fast path: `every A -> B` with f / g as term lists on the
     // events' own columns, plain-copy select items, <= 2 captures, <= 512
     // keys per bucket (CEP_NO_CF=1 forces the general path)
@@ -1210,9 +1223,11 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
   constexpr int64_t kTile = kFilterThreads * kFilterItems;
   const int64_t ntiles = (rows.n + kTile - 1) / kTile;
   if (ntiles == 0) return CEP_OK;
-  if (!dev_ensure(&a->tile_state, (size_t)ntiles * 8, a->stream, false))
+  // look-back words for k_filter's or k_filterc's (smaller) tiles
+  const int64_t nflags = std::max<int64_t>(ntiles, (rows.n + filterc_rows_per_tile() - 1) / filterc_rows_per_tile());
+  if (!dev_ensure(&a->tile_state, (size_t)nflags * 8, a->stream, false))
     return fail(a, CEP_E_DEVICE, "out of device memory (tile state)");
-  hipMemsetAsync(a->tile_state.p, 0, (size_t)ntiles * 8, a->stream);
+  hipMemsetAsync(a->tile_state.p, 0, (size_t)nflags * 8, a->stream);
   hipMemsetAsync(a->ticket.p, 0, 16, a->stream);
   FilterArgs fa{};
   fa.rows = rows;
@@ -1224,10 +1239,47 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
   fa.tile_state = (unsigned long long*)a->tile_state.p;
   fa.ticket = (unsigned int*)a->ticket.p;
   fa.err = (unsigned int*)a->err.p;
-  LaunchTimer t(a, CEP_K_FILTER);
   bool vm = q.filter.off >= 0 && q.filter_terms.n < 0;
   for (auto& it : q.select) vm |= it.src < SRC_REC || it.src >= SRC_TS;
-  launch_filter(fa, ntiles, vm, a->stream);
+  // k_filterc (filter.hip): term-list predicate over at most 3 distinct
+  // columns, plain projection, pair loads aligned (8-byte columns at 16
+  // bytes, 4-byte at 8, 1-byte at 2 from the slice's first row, which is
+  // even).  CEP_NO_FILTERC=1 keeps k_filter.
+  static const bool no_fc = std::getenv("CEP_NO_FILTERC") != nullptr;
+  bool fc = !vm && !no_fc && (rows.row0 & 1) == 0;
+  if (fc) {
+    fa.npref = 0;
+    for (int i = 0; fc && i < std::max(0, q.filter_terms.n); ++i) {
+      const int c = q.filter_terms.t[i].col;
+      int slot = -1;
+      for (int k = 0; k < fa.npref; ++k)
+        if (fa.pcol[k] == c) slot = k;
+      if (slot < 0) {
+        if (fa.npref == 3) {
+          fc = false;
+          break;
+        }
+        slot = fa.npref;
+        fa.pcol[fa.npref++] = c;
+      }
+      fa.fslot[i] = slot;
+    }
+    if (fa.npref == 0) fa.pcol[fa.npref++] = 0;   // no predicate: one (unused) column
+    auto al = [&](const void* ptr, int w) {
+      return (((uintptr_t)ptr + (uintptr_t)(rows.row0 * w)) & (uintptr_t)(2 * w - 1)) == 0;
+    };
+    for (int k = 0; fc && k < fa.npref; ++k)
+      fc = al(rows.cols.p[fa.pcol[k]], type_width(rows.cols.t[fa.pcol[k]]));
+    if (fc && rows.stream) fc = al(rows.stream, 1);
+  }
+  LaunchTimer t(a, CEP_K_FILTER);
+  if (fc) {
+    const int64_t tr = filterc_rows_per_tile();
+    const int64_t nt = (rows.n + tr - 1) / tr;
+    launch_filterc(fa, nt, a->stream);
+  } else {
+    launch_filter(fa, ntiles, vm, a->stream);
+  }
   return CEP_OK;
 }
 
@@ -1590,10 +1642,20 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
     wa.kstride = rt.kstride;
     wa.out = out_args(o, q);
     wa.err = pa.err;
+    const bool pool = q.nfa && rt.kext.p;
+    if (pool) {
+      wa.kext = (uint64_t*)rt.kext.p;
+      wa.pool_rd = (const uint64_t*)rt.pool[rt.pool_side].p;
+      wa.pool_wr = (uint64_t*)rt.pool[rt.pool_side ^ 1].p;
+      wa.pool_cursor = (unsigned long long*)rt.pool_cur.p;
+      wa.pool_cap = (uint64_t)rt.pool_cap;
+      hipMemsetAsync(rt.pool_cur.p, 0, 8, a->stream);
+    }
     {
       LaunchTimer t(a, CEP_K_WALK);
       launch_walk(wa, P, rt.walk_vm, a->stream);
     }
+    if (pool) rt.pool_side ^= 1;   // this launch's write pool holds every run now
     hipEventRecord(rt.walk_done[b], a->stream);
     rt.used[b] = true;
   }

@@ -72,6 +72,8 @@ enum : uint32_t {
 constexpr uint32_t kHdrOvf = 1u << 9;
 
 // ---------------------------------------------------------------- filter --
+constexpr int kPref = 4;   // prefetched column slots of the fast paths
+
 struct FilterArgs {
   RowsArgs rows;
   VmArgs vm;
@@ -82,6 +84,10 @@ struct FilterArgs {
   unsigned long long* tile_state;   // decoupled look-back words (zeroed per launch)
   unsigned int* ticket;             // tile ticket counter (zeroed per launch)
   unsigned int* err;
+  // k_filterc (filter.hip): the predicate's distinct columns and each term's slot
+  int32_t npref;
+  int32_t pcol[kPref];
+  int32_t fslot[kMaxTerms];
 };
 
 // ------------------------------------------------------- keyed pattern --
@@ -135,7 +141,6 @@ struct PatternArgs {
 // Fast partition path: every column the pattern reads (key, f / g term
 // columns, carried columns; at most kPref) is loaded for all of a lane's rows
 // up front with 16-byte loads, so the tile's loads are in flight together.
-constexpr int kPref = 4;
 constexpr int kPfRec = 2;        // carried words per record on the fast path
 struct PrefPlan {
   int32_t n = -1;                // -1: generic path (per-use loads)
@@ -225,6 +230,15 @@ struct WalkArgs {
   uint64_t* stamps;            // diagnostics (CEP_STAMPS=1): per block 16 s_memtime stamps
   OutArgs out;
   unsigned int* err;
+  // N-state patterns / sequences: partial lists longer than pending_slots
+  // (khdr bit kHdrOvf) keep slots [S, n) in a run of the pending pool, the
+  // closed-form layout (kext = n | pool offset << 32, runs in pool_rd at
+  // launch start; bit 31 of kext: the run is in pool_wr).  nullptr: no pool.
+  uint64_t* kext;
+  const uint64_t* pool_rd;
+  uint64_t* pool_wr;
+  unsigned long long* pool_cursor;
+  uint64_t pool_cap;           // slots per pool
 };
 
 // ------------------------------------------ closed-form fast path (cf_kernels.hip) --
@@ -549,6 +563,10 @@ void launch_route_keys(const RouteKeyArgs& a, hipStream_t s);
 void launch_hot_match(const HotArgs& a, hipStream_t s);
 void launch_hot_update(const HotArgs& a, int diverted, hipStream_t s);
 void launch_filter(const FilterArgs& a, int64_t ntiles, bool vm, hipStream_t s);
+// coalesced compaction filter (filter.hip): term-list predicate over <= 3
+// columns, plain projection; rows per tile
+void launch_filterc(const FilterArgs& a, int64_t ntiles, hipStream_t s);
+int filterc_rows_per_tile();
 void launch_partition(const PartArgs& a, int64_t ntiles, bool vm, hipStream_t s);
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,
                   unsigned long long* dcount, uint64_t* out, hipStream_t s);

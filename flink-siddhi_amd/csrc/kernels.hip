@@ -1358,11 +1358,11 @@ __device__ uint32_t agg_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int k, i
 // one by one (a lane's rows of one event stay in creation order).
 template <bool kVm>
 __device__ __forceinline__ bool nfa_cond(const WalkArgs& a, uint64_t* R, int j, uint32_t role,
-                                         const uint64_t* slot, const uint64_t* rec, int64_t ts_base) {
+                                         const uint64_t* slot, int64_t st, const uint64_t* rec, int64_t ts_base) {
   const PatternArgs& p = a.pat;
   if (!((role >> j) & 1u)) return false;
   if (!kVm || p.st_walk[j] < 0) return true;
-  const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, a.kstride};
+  const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, st};
   bool isnull = false;
   const uint64_t v = eval_env(a.vm, p.st_walk[j], R, env, &isnull);
   return !isnull && (v & 1u);
@@ -1379,11 +1379,11 @@ __device__ __forceinline__ void nfa_collect(const PatternArgs& p, uint64_t* slot
 }
 
 template <bool kVm>
-__device__ __forceinline__ void nfa_emit(const WalkArgs& a, uint64_t* R, const uint64_t* slot,
+__device__ __forceinline__ void nfa_emit(const WalkArgs& a, uint64_t* R, const uint64_t* slot, int64_t st,
                                          const uint64_t* rec, int64_t ts_base, int64_t seq_base,
                                          int64_t kl) {
   const PatternArgs& p = a.pat;
-  const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, a.kstride};
+  const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, st};
   const unsigned long long pos = atomicAdd(a.out.count, 1ull);
   emit_row<kVm>(a, R, env, key_value(p, kl), rec_seq(rec, seq_base), pos);
 }
@@ -1397,21 +1397,52 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
   const int64_t idx = (int64_t)bucket * kpb + k;
   const int64_t kl = ((int64_t)k << p.buckets_log2) | bucket;
   uint64_t* sl = a.kslot + idx;
-#define NSLOT(j) (sl + (int64_t)(j) * sw * ks)
+  uint32_t hdr = L.khdr[k];
+  const bool ovf0 = (hdr & kHdrOvf) != 0;
+  const uint64_t ext0 = ovf0 ? a.kext[idx] : 0ull;
+  int n = ovf0 ? (int)(ext0 & 0x7fffffffull) : (int)(hdr & 0xffu);
+  bool started = ((hdr >> 8) & 1u) != 0;
+  // Working storage.  Inline: list [0, S), staging [S, 2S), word stride ks.
+  // A list that may outgrow S in this window (n + its records > S: each
+  // record adds at most one partial) works in one pool run instead: list
+  // [0, M), staging [M, 2M), word stride 1; it is written back in the
+  // at-rest layout (inline [0, S) + tail run) when the key is done.
+  uint64_t* run = nullptr;
+  unsigned long long roff = 0;
+  int64_t st = ks;
+  int CAP = S;
+  const int64_t M = (int64_t)n + (int64_t)(L.kstart[k + 1] - L.kstart[k]);
+  if (M > S && a.pool_wr) {
+    const unsigned long long need = 2ull * (unsigned long long)M;
+    const unsigned long long o = atomicAdd(a.pool_cursor, need);
+    if (o + need > a.pool_cap) {
+      set_err(a.err, ERR_POOL);
+      if (ovf0) return;   // the key keeps its state; the error is reported
+    } else {
+      roff = o;
+      run = a.pool_wr + o * (uint64_t)sw;
+      st = 1;
+      CAP = (int)M;
+      const uint64_t* tail =
+          ovf0 ? (((ext0 >> 31) & 1ull) ? (const uint64_t*)a.pool_wr : a.pool_rd) + (ext0 >> 32) * (uint64_t)sw
+               : nullptr;
+      for (int j = 0; j < n; ++j)
+        for (int x = 0; x < sw; ++x)
+          run[(int64_t)j * sw + x] = j < S ? sl[((int64_t)j * sw + x) * ks] : tail[(int64_t)(j - S) * sw + x];
+    }
+  }
+#define NSLOT(j) (run ? run + (int64_t)(j) * sw : sl + (int64_t)(j) * sw * ks)
   auto copy_slot = [&](int dst, int src) {
     if (dst == src) return;
-    for (int x = 0; x < sw; ++x) NSLOT(dst)[x * ks] = NSLOT(src)[x * ks];
+    for (int x = 0; x < sw; ++x) NSLOT(dst)[x * st] = NSLOT(src)[x * st];
   };
   auto settle = [&](uint64_t* slot, int j, int c, const uint64_t* rec) -> bool {
     // returns whether the partial survives; emits when complete
     const bool done = c >= p.st_min[j] && p.st_tail_opt[j];
     if (!done) return true;
-    nfa_emit<kVm>(a, R, slot, rec, ts_base, seq_base, kl);
+    nfa_emit<kVm>(a, R, slot, st, rec, ts_base, seq_base, kl);
     return j == N - 1 && (p.st_max[j] < 0 || c < p.st_max[j]);
   };
-  uint32_t hdr = L.khdr[k];
-  int n = (int)(hdr & 0xffu);
-  bool started = ((hdr >> 8) & 1u) != 0;
   for (uint32_t q = L.kstart[k]; q < L.kstart[k + 1]; ++q) {
     const uint64_t* rec = a.recs + (int64_t)L.wrec[L.sorted[q]] * rw;
     const uint64_t h = rec[0];
@@ -1420,45 +1451,45 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
     const int64_t ts = rec_ts(rec, ts_base);
     int m = 0;
     if (!p.nfa_seq) {
-      int nf = 0;   // advanced partials, staged in slots [S, 2S)
+      int nf = 0;   // advanced partials, staged in slots [CAP, 2 CAP)
       for (int i = 0; i < n; ++i) {
         uint64_t* si = NSLOT(i);
-        const int j = (int)(si[ks] & 0xffu);
+        const int j = (int)(si[st] & 0xffu);
         if (p.st_stream[j] != stream) { copy_slot(m++, i); continue; }
         if (p.within >= 0) {
           const int64_t d = ts - (int64_t)si[0];
           if ((d < 0 ? -d : d) > p.within) continue;   // expired: dropped
         }
-        if (!nfa_cond<kVm>(a, R, j, role, si, rec, ts_base)) { copy_slot(m++, i); continue; }
+        if (!nfa_cond<kVm>(a, R, j, role, si, st, rec, ts_base)) { copy_slot(m++, i); continue; }
         if (j + 1 == N) {
-          nfa_collect(p, si, ks, j, 1, rec);
-          nfa_emit<kVm>(a, R, si, rec, ts_base, seq_base, kl);   // consumed
+          nfa_collect(p, si, st, j, 1, rec);
+          nfa_emit<kVm>(a, R, si, st, rec, ts_base, seq_base, kl);   // consumed
           continue;
         }
-        copy_slot(S + nf, i);
-        nfa_collect(p, NSLOT(S + nf), ks, j + 1 - 1, 1, rec);
-        NSLOT(S + nf)[ks] = (uint64_t)(j + 1);
+        copy_slot(CAP + nf, i);
+        nfa_collect(p, NSLOT(CAP + nf), st, j + 1 - 1, 1, rec);
+        NSLOT(CAP + nf)[st] = (uint64_t)(j + 1);
         ++nf;
       }
       if (p.st_stream[0] == stream && (p.every || !started) &&
-          nfa_cond<kVm>(a, R, 0, role, nullptr, rec, ts_base)) {
+          nfa_cond<kVm>(a, R, 0, role, nullptr, st, rec, ts_base)) {
         started = true;
-        uint64_t* ns = NSLOT(S + nf);
+        uint64_t* ns = NSLOT(CAP + nf);
         ns[0] = (uint64_t)ts;
-        for (int x = 2; x < sw; ++x) ns[x * ks] = p.cap_null[x - 2];
-        nfa_collect(p, ns, ks, 0, 1, rec);
+        for (int x = 2; x < sw; ++x) ns[x * st] = p.cap_null[x - 2];
+        nfa_collect(p, ns, st, 0, 1, rec);
         if (N == 1) {
-          nfa_emit<kVm>(a, R, ns, rec, ts_base, seq_base, kl);
+          nfa_emit<kVm>(a, R, ns, st, rec, ts_base, seq_base, kl);
         } else {
-          ns[ks] = 1;
+          ns[st] = 1;
           ++nf;
         }
       }
-      if (m + nf > S) {
+      if (m + nf > CAP) {
         set_err(a.err, ERR_PENDING);
-        nf = S - m;
+        nf = CAP - m;
       }
-      for (int f = 0; f < nf; ++f) copy_slot(m + f, S + f);
+      for (int f = 0; f < nf; ++f) copy_slot(m + f, CAP + f);
       n = m + nf;
     } else {
       for (int i = 0; i < n; ++i) {
@@ -1467,17 +1498,17 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
           const int64_t d = ts - (int64_t)si[0];
           if ((d < 0 ? -d : d) > p.within) continue;
         }
-        const uint64_t jc = si[ks];
+        const uint64_t jc = si[st];
         const int j = (int)(jc & 0xffu), c = (int)(jc >> 8);
         bool keep = false;
         if (p.st_stream[j] == stream && (p.st_max[j] < 0 || c < p.st_max[j]) &&
-            nfa_cond<kVm>(a, R, j, role, si, rec, ts_base)) {
-          nfa_collect(p, si, ks, j, c + 1, rec);              // stay in the count state
+            nfa_cond<kVm>(a, R, j, role, si, st, rec, ts_base)) {
+          nfa_collect(p, si, st, j, c + 1, rec);              // stay in the count state
           keep = settle(si, j, c + 1, rec);
         } else if (c >= p.st_min[j]) {
           for (int j2 = j + 1; j2 < N; ++j2) {                // move on, skipping optional states
-            if (p.st_stream[j2] == stream && nfa_cond<kVm>(a, R, j2, role, si, rec, ts_base)) {
-              nfa_collect(p, si, ks, j2, 1, rec);
+            if (p.st_stream[j2] == stream && nfa_cond<kVm>(a, R, j2, role, si, st, rec, ts_base)) {
+              nfa_collect(p, si, st, j2, 1, rec);
               keep = settle(si, j2, 1, rec);
               break;
             }
@@ -1487,15 +1518,15 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
         if (keep) copy_slot(m++, i);                          // else discarded (contiguity)
       }
       if (p.st_stream[0] == stream && (p.every || !started) &&
-          nfa_cond<kVm>(a, R, 0, role, nullptr, rec, ts_base)) {
+          nfa_cond<kVm>(a, R, 0, role, nullptr, st, rec, ts_base)) {
         started = true;
-        if (m >= S) {
+        if (m >= CAP) {
           set_err(a.err, ERR_PENDING);
         } else {
           uint64_t* ns = NSLOT(m);
           ns[0] = (uint64_t)ts;
-          for (int x = 2; x < sw; ++x) ns[x * ks] = p.cap_null[x - 2];
-          nfa_collect(p, ns, ks, 0, 1, rec);
+          for (int x = 2; x < sw; ++x) ns[x * st] = p.cap_null[x - 2];
+          nfa_collect(p, ns, st, 0, 1, rec);
           if (settle(ns, 0, 1, rec)) ++m;
         }
       }
@@ -1503,11 +1534,48 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
     }
   }
 #undef NSLOT
-  const uint32_t nh = (uint32_t)n | ((started ? 1u : 0u) << 8);
+  bool ovf = false;
+  if (run) {   // back to the at-rest layout: inline [0, S), tail [S, n) in place in the run
+    for (int j = 0; j < n && j < S; ++j)
+      for (int x = 0; x < sw; ++x) sl[((int64_t)j * sw + x) * ks] = run[(int64_t)j * sw + x];
+    if (n > S) {
+      ovf = true;
+      a.kext[idx] = (uint64_t)(uint32_t)n | (1ull << 31) | ((uint64_t)(roff + (unsigned long long)S) << 32);
+    }
+  } else if (ovf0) {   // unreachable (an overflowed list always works in a run)
+    ovf = true;
+  }
+  const uint32_t nh = (uint32_t)(ovf ? S : n) | ((started ? 1u : 0u) << 8) | (ovf ? kHdrOvf : 0u);
   L.khdr[k] = nh;
   a.khdr[idx] = nh;
 }
 
+// Kernel end (N-state walk): a key's overflow tail still in the read pool
+// moves to the write pool (the host swaps the pools per launch); kext then
+// names the run in what the next launch reads.
+__device__ void nfa_settle_runs(const WalkArgs& a, WalkLds& L, int bucket, int kpb) {
+  const int S = a.pat.pending_slots, sw = a.pat.slot_words;
+  for (int k = threadIdx.x; k < kpb; k += kWalkThreads) {
+    if (!(L.khdr[k] & kHdrOvf)) continue;
+    const int64_t idx = (int64_t)bucket * kpb + k;
+    uint64_t e = a.kext[idx];
+    const uint64_t n = e & 0x7fffffffull;
+    uint64_t off = e >> 32;
+    if (!((e >> 31) & 1ull)) {
+      const unsigned long long cnt = n - (uint64_t)S;
+      const unsigned long long o = atomicAdd(a.pool_cursor, cnt);
+      if (o + cnt > a.pool_cap) {
+        set_err(a.err, ERR_POOL);
+        continue;
+      }
+      const uint64_t* src = a.pool_rd + off * (uint64_t)sw;
+      uint64_t* dst = a.pool_wr + o * (uint64_t)sw;
+      for (uint64_t i = 0; i < cnt * (uint64_t)sw; ++i) dst[i] = src[i];
+      off = o;
+    }
+    a.kext[idx] = n | (off << 32);
+  }
+}
 
 }  // namespace
 
@@ -1534,10 +1602,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
   // this bucket's per-key headers: kpb consecutive words (bucket-major index)
   for (int k = tid; k < kpb; k += kWalkThreads) {
     const uint32_t h = a.khdr[(int64_t)bucket * kpb + k];
-    // a list that overflowed into the pending pool (closed-form path) does
-    // not fit this walk's per-key LDS lists
-    if (h & kHdrOvf) set_err(a.err, ERR_PENDING);
-    L.khdr[k] = h & ~kHdrOvf;
+    // a list that overflowed into the pending pool: the N-state walk works on
+    // it (nfa_key); the other walks keep per-key lists of pending_slots
+    if ((h & kHdrOvf) && !(kVm && p.nfa_mode && a.kext)) {
+      set_err(a.err, ERR_PENDING);
+      L.khdr[k] = h & ~kHdrOvf;
+    } else {
+      L.khdr[k] = h;
+    }
   }
 
   // segment starts and sizes -> exclusive prefix over tiles
@@ -1881,6 +1953,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(WalkArgs a) {
     if (t1 < ntiles) __syncthreads();
     t0 = t1;
   }
+  if constexpr (kVm)
+    if (p.nfa_mode && a.kext) nfa_settle_runs(a, L, bucket, kpb);
 }
 
 void launch_walk(const WalkArgs& a, int nbuckets, bool vm, hipStream_t s) {
