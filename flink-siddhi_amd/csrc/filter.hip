@@ -25,10 +25,16 @@ namespace cep {
 
 namespace {
 
-constexpr int kFcThreads = 256;
+#ifndef FC_THREADS
+#define FC_THREADS 1024
+#endif
+constexpr int kFcThreads = FC_THREADS;
 constexpr int kFcWaves = kFcThreads / 64;
 #ifndef FC_PAIRS
 #define FC_PAIRS 4
+#endif
+#ifndef FC_REGCOLS
+#define FC_REGCOLS 4
 #endif
 #ifndef FC_MINW
 #define FC_MINW 4
@@ -36,7 +42,7 @@ constexpr int kFcWaves = kFcThreads / 64;
 constexpr int kFcPairs = FC_PAIRS;               // row pairs per lane
 constexpr int kFcWaveRows = 64 * 2 * kFcPairs;   // 512
 constexpr int kFcTile = kFcWaves * kFcWaveRows;  // 2048
-constexpr int kFcRegCols = 8;                    // projected columns loaded ahead of the look-back
+constexpr int kFcRegCols = FC_REGCOLS;                    // projected columns loaded ahead of the look-back
 constexpr uint64_t kFcStatusShift = 62;
 constexpr uint64_t kFcValueMask = (1ull << 62) - 1;
 
@@ -73,9 +79,13 @@ __global__ __launch_bounds__(kFcThreads, FC_MINW) void k_filterc(FilterArgs a) {
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_prefix;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef FC_NOTICKET   // experiment: tiles in dispatch order (the look-back's spin limit bounds a stall)
+  const int64_t tile = blockIdx.x;
+#else
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
   __syncthreads();
   const int64_t tile = s_tile;
+#endif
   const int64_t n = a.rows.n;
   const int64_t wrow0 = tile * kFcTile + (int64_t)wave * kFcWaveRows;   // slice-relative
   const int64_t brow0 = a.rows.row0 + wrow0;                            // batch row

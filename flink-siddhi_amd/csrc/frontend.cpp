@@ -18,6 +18,7 @@
 #include "frontend.h"
 
 #include <cctype>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -1431,10 +1432,25 @@ void compile_nfa(CompiledApp* app, QueryAst& q) {
   app->queries.push_back(out);
 }
 
+// Whether e reads an attribute qualified by `alias` (before binding).
+bool refs_alias(const ExprP& e, const std::string& alias) {
+  if (!e) return false;
+  if (e->k == Expr::ATTR && e->ref == alias) return true;
+  for (auto& a : e->args)
+    if (refs_alias(a, alias)) return true;
+  return false;
+}
+
 void compile_pattern(CompiledApp* app, QueryAst& q) {
   bool counts = false;
   for (auto& s : q.states) counts |= s.min_count != 1 || s.max_count != 1;
   if (q.sequence || q.states.size() != 2 || counts) return compile_nfa(app, q);
+  // s2's condition reads s1: the N-state walk (its pending lists continue in
+  // the pending pool, so no key runs out of slots); CEP_PAIR_WALK=1 keeps the
+  // two-state walk (lists of pending_slots)
+  static const bool pair_walk = std::getenv("CEP_PAIR_WALK") != nullptr;
+  if (!pair_walk && !q.states[0].alias.empty() && refs_alias(q.states[1].cond, q.states[0].alias))
+    return compile_nfa(app, q);
   for (auto& s : q.states) {
     if (app->input_index(s.stream) < 0)
       fail(CEP_E_UNDEFINED_STREAM, "stream " + s.stream + " is not defined");

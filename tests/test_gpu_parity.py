@@ -68,6 +68,24 @@ def test_pattern_condition_on_s1():
     assert m > 20
 
 
+def test_pattern_condition_on_s1_long_pending_lists():
+    # an s1-dependent condition keeps ~150 live partials
+    # per key (16 keys, 1 event/ms, 10 s window; B[id > s1.id + 47] is rare)
+    # with 16 inline slots: the N-state walk continues the lists in the
+    # pending pool instead of failing with CEP_E_CAPACITY
+    plan = EV2 + ("partition with (k of A, k of B) begin "
+                  "from every s1=A[price > 0.2] -> s2=B[id > s1.id + 47] within 10 sec "
+                  "select s1.id as i1, s2.id as i2, s1.price as p1, s2.ts as t insert into O; end;")
+    w = workload.generate(0, 40000, 16, rate=1)
+    a = (w["stream"] == 0) & (w["price"] > 0.2)
+    per_key = max(int(((w["k"] == k) & a & (w["ts"] < w["ts"][0] + 10000)).sum()) for k in range(16))
+    assert per_key >= 40
+    want = oracle_run(plan, workload_events(w)).get("O", [])
+    got = run_engine(plan, w, batches=2, pending_slots=16, chunk_events=8192)
+    assert len(want) > 200
+    assert_same_rows(got, want, plan)
+
+
 def test_pattern_without_every_is_one_shot_per_key():
     plan = EV2 + ("partition with (k of A, k of B) begin "
                   "from s1=A[price > 0.9] -> s2=B[id == 7] select s1.k as k, s2.ts as t "
