@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--ordered", action="store_true",
                     help="with --deliver: ordered_output=1, rows sorted into Siddhi's global emission "
                          "order on the device before the D2H (the drop-in default)")
+    ap.add_argument("--with-seq", action="store_true",
+                    help="with --deliver: also deliver each row's arrival number (omitted by default, as the "
+                         "reference's output handler does not read it)")
     ap.add_argument("--parity-steps", type=int, default=4,
                     help="config 5: steps of the stream the parity check covers (fresh state)")
     return ap.parse_args()
@@ -411,6 +414,10 @@ def main():
         del w
     if args.ordered:
         opts["ordered_output"] = 1
+    if args.deliver and not args.with_seq:
+        # the reference's StreamOutputHandler never reads the arrival number:
+        # it is not gathered or copied to the host (cep_options.omit_seq)
+        opts["omit_seq"] = 1
     rt = fs.SiddhiAppRuntime(plan, **opts)
 
     # Inputs for every step, generated on the device before the timed region.
