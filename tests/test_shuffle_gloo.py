@@ -102,3 +102,41 @@ def test_key_shuffle_gloo_matches_single_process(side, padded, world):
     want = oracle_run(PLAN, workload_events(w)).get("O", [])
     assert len(want) > 50
     assert merged == want
+
+
+def _reinit_main(rank, world, ports, q):
+    # the side count group is cached per default group object; a
+    # destroyed and re-initialised world must get a group of its own
+    os.environ["CEP_COUNT_GROUP"] = "side"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    got = []
+    try:
+        for it, port in enumerate(ports):
+            os.environ["MASTER_PORT"] = str(port)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            counts = [rank * 10 + d + it for d in range(world)]
+            got.append(shuffle.exchange_counts(counts))
+            g = shuffle._count_group()
+            assert g is not None and g != "device"
+            dist.destroy_process_group()
+        q.put((rank, got))
+    except Exception as e:   # reported to the parent
+        q.put((rank, repr(e)))
+
+
+def test_count_group_survives_world_reinit():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ports = [_free_port(), _free_port()]
+    procs = [ctx.Process(target=_reinit_main, args=(r, world, ports, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+        for it in range(2):
+            assert res[r][it] == [s * 10 + r + it for s in range(world)]
