@@ -40,11 +40,30 @@ constexpr uint16_t kNoB = 0xffff;
 constexpr int kCfStageBytes = (kCfTile / 8192 * 20 + 36) * 1024;    // a tile keeps ~1/3 of its rows at config 3
 
 // Diagnostics (CEP_STAMPS=1): s_memtime at phase i of block b.
+#ifdef CF_WAVESTAMP
+#define CF_STAMP(i) do { } while (0)
+#else
 #define CF_STAMP(i)                                                                 \
   do {                                                                              \
     if (a.stamps && threadIdx.x == 0 && blockIdx.x < 4096)                          \
       a.stamps[(int64_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime();      \
   } while (0)
+#endif
+
+// Diagnostics build (-DCF_WAVESTAMP, CEP_STAMPS=1): window 0 of each block,
+// slot 0 = wave 0 after the output-scan barrier, slots 1-8 = each wave at the
+// end of its key-lane commit, slots 9-15 = waves 0-6 at the end of the
+// record emission (which wave holds the window-end barrier, and why).
+#ifdef CF_WAVESTAMP
+#define CF_WSTAMP(slot)                                                             \
+  do {                                                                              \
+    if (a.stamps && (threadIdx.x & 63) == 0 && blockIdx.x < 4096 && wi == 0 &&     \
+        (slot) < 16)                                                                \
+      a.stamps[(int64_t)blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memtime();  \
+  } while (0)
+#else
+#define CF_WSTAMP(slot) do { } while (0)
+#endif
 
 // Diagnostics (CEP_STAMPS=1 CEP_ABLATE=256): event counters of the walk (last launch).
 #define CF_COUNT(i, v)                                                                       \
@@ -981,7 +1000,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       if (tid == 0) { CF_COUNT(1, total); CF_COUNT(5, 1); }
     }
     lds_barrier();
+#ifndef CF_WAVESTAMP
     CF_STAMP(wi * 8 + 5);
+#else
+    if ((threadIdx.x >> 6) == 0) CF_WSTAMP(0);
+#endif
     const unsigned long long base = L.base;
     const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
 
@@ -1091,7 +1114,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       if (nn > S) ovo = noff | kOvoWr;
       n = nn;
     }
+#ifndef CF_WAVESTAMP
     CF_STAMP(wi * 8 + 6);
+#else
+    CF_WSTAMP(1 + (int)(threadIdx.x >> 6));
+#endif
 
     // ---- emit record matches (lane per sorted position; LDS reads + stores)
 #pragma unroll 1
@@ -1115,7 +1142,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
               NW > 0 ? L.scap[0][nb] : 0ull, NW > 1 ? L.scap[NW > 1 ? 1 : 0][nb] : 0ull, bts,
               seq_base + (int64_t)L.sseq[nb]);
     }
+#ifndef CF_WAVESTAMP
     CF_STAMP(wi * 8 + 7);
+#else
+    CF_WSTAMP(9 + (int)(threadIdx.x >> 6));
+#endif
     if (over) {
       piece += nw;
       if (piece >= L.seg[t0 + 1] - L.seg[t0]) {

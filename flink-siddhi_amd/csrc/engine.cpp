@@ -1997,6 +1997,24 @@ void cep_destroy(cep_app* a) {
       for (int i = 1; i < 16; ++i) std::fprintf(stderr, " d%d=%.0f(%d)", i, dn[i] ? dsum[i] / dn[i] : 0.0, dn[i]);
       std::fprintf(stderr, "\n");
     }
+    if (std::getenv("CEP_WAVESTAMP")) {   // -DCF_WAVESTAMP build: per-wave ends vs slot 0
+      double m[16] = {0};
+      int c[16] = {0};
+      for (int b = 0; b < nb; ++b) {
+        const uint64_t* t = &st[(size_t)b * 16];
+        if (!t[0]) continue;
+        for (int i = 1; i < 16; ++i)
+          if (t[i]) {
+            m[i] += (double)(int64_t)(t[i] - t[0]);
+            ++c[i];
+          }
+      }
+      std::fprintf(stderr, "[cep wavestamps] commit end per wave:");
+      for (int i = 1; i <= 8; ++i) std::fprintf(stderr, " w%d=%.0f", i - 1, c[i] ? m[i] / c[i] : 0.0);
+      std::fprintf(stderr, "\n[cep wavestamps] emission end per wave:");
+      for (int i = 9; i < 16; ++i) std::fprintf(stderr, " w%d=%.0f", i - 9, c[i] ? m[i] / c[i] : 0.0);
+      std::fprintf(stderr, "\n");
+    }
     std::fprintf(stderr, "[cep stamps] walk window0 ticks/block:");
     for (int i = 1; i < 8; ++i) std::fprintf(stderr, " p%d=%.0f", i, sum[i] / nb);
     std::fprintf(stderr, "\n[cep stamps] walk window1 (%d blocks):", n1);
