@@ -508,9 +508,11 @@ struct CfWalkLds {
   };
   union {
     uint32_t wrec[WIN];                // arena record index per window slot (gather, reload)
-    uint64_t pcache[WIN / 2];          // from p4: key lanes' pending slots >= 2 (ts, captures)
+    uint64_t pcache[WIN / 2];          // from p4: key lanes' pending slots >= 2 (ts, captures);
+                                       // its last kCfOmap / 4 words hold omap (record-match positions)
   };
   uint32_t pc_used;                    // pcache words handed out this window
+  uint32_t nrec;                       // record matches of the window (omap entries)
   union {
     uint64_t kent[WIN];                // seq << 20 | key << 11 | slot, grouped by key
     uint64_t scap[NW > 0 ? NW : 1][WIN];   // sorted: physical carried words
@@ -533,6 +535,10 @@ struct CfWalkLds {
   uint32_t scratch2[kCfWalkThreads / 64 + 1];   // the output scan's (no tail barrier)
   unsigned long long base;
 };
+
+// Record matches a window lists for the compacted emission (lane per output
+// row): the top of the pcache region, which holds no key's slots then.
+constexpr int kCfOmap = 1024;
 
 // One output row.  acap = the A's logical captures, b0 / b1 = the completing
 // B's physical words, bts / seq = its event ts and arrival number.
@@ -879,7 +885,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     if (fill) {
       const uint32_t need = (uint32_t)((ni - 2) * cw);
       pco = atomicAdd(&L.pc_used, need);
-      if (pco + need <= (uint32_t)(WIN / 2)) {
+      if (pco + need <= (uint32_t)(WIN / 2 - kCfOmap / 4)) {
         pcb = pco;
         cn = ni - 2;
       }
@@ -968,7 +974,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     lds_barrier();
     CF_STAMP(wi * 8 + 4);
 
-    // ---- match flag per sorted position (+ carried matches at run start)
+    // ---- match flag per sorted position (+ carried matches at run start);
+    // one scan yields both the output offsets (low 20 bits) and each record
+    // match's rank among the window's record matches (bits 20-31), which
+    // lists it in omap for the compacted emission
+    uint16_t* omap = (uint16_t*)&L.pcache[WIN / 2 - kCfOmap / 4];
     {
       uint32_t vals[PER];
       uint32_t sum = 0;
@@ -982,7 +992,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
           const uint16_t nb = L.nextb[q];
           if (((kr >> 12) & ROLE_A) && nb != kNoB) {
             const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
-            val = (W < 0 || (d < 0 ? -d : d) <= W) ? 1u : 0u;
+            val = (W < 0 || (d < 0 ? -d : d) <= W) ? (1u << 20) | 1u : 0u;
           }
           if (q == L.kstart[kbuf][k]) val += L.cm[k];
         }
@@ -993,11 +1003,17 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       uint32_t off = bscan<NT, false>(sum, L.scratch2, &total);
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        L.v[tid * PER + i] = (uint16_t)off;
+        const uint32_t q = tid * PER + i;
+        L.v[q] = (uint16_t)(off & 0xfffffu);
+        if ((vals[i] >> 20) && (off >> 20) < (uint32_t)kCfOmap) omap[off >> 20] = (uint16_t)q;
         off += vals[i];
       }
-      if (tid == 0) L.base = total ? atomicAdd(a.out.count, (unsigned long long)total) : 0ull;
-      if (tid == 0) { CF_COUNT(1, total); CF_COUNT(5, 1); }
+      const uint32_t rows = total & 0xfffffu;
+      if (tid == 0) {
+        L.base = rows ? atomicAdd(a.out.count, (unsigned long long)rows) : 0ull;
+        L.nrec = total >> 20;
+      }
+      if (tid == 0) { CF_COUNT(1, rows); CF_COUNT(5, 1); }
     }
     lds_barrier();
 #ifndef CF_WAVESTAMP
@@ -1120,10 +1136,15 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     CF_WSTAMP(1 + (int)(threadIdx.x >> 6));
 #endif
 
-    // ---- emit record matches (lane per sorted position; LDS reads + stores)
+    // ---- emit record matches: lane per output row from omap (consecutive
+    // lanes write consecutive rows, every lane busy), or lane per sorted
+    // position when the window has more record matches than omap lists
+    const uint32_t nrec = L.nrec;
+    const bool compact = nrec <= (uint32_t)kCfOmap && !(a.ablate & 8);   // ablate 8: per position
+    const uint32_t nemit = compact ? nrec : (uint32_t)(PER * NT);
 #pragma unroll 1
-    for (int i = 0; i < PER; ++i) {
-      const uint32_t q = tid + i * NT;
+    for (uint32_t j = tid; j < nemit; j += NT) {
+      const uint32_t q = compact ? (uint32_t)omap[j] : j;
       if (q >= nw || (a.ablate & 4)) continue;   // ablate 4 (diagnostics): no record-match stores
       const uint32_t kr = L.skr[q];
       const uint16_t nb = L.nextb[q];
