@@ -898,31 +898,94 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       pv1[u] = (ld && c1) ? sl_ld(j, 2) : 0ull;
       pv2[u] = (ld && c2) ? sl_ld(j, 3) : 0ull;
     }
-    // ---- per sorted position: next B of the run, first / last B, last A
-#pragma unroll 1
-    for (int i = 0; i < PER; ++i) {
-      const uint32_t s = tid + i * NT;
-      if (s >= nw) continue;
-      const uint32_t kr = L.skr[s];
-      const uint32_t k = kr & 0xfffu, role = kr >> 12;
-      const uint32_t r1 = L.kstart[kbuf][k + 1];
-      uint16_t nb = kNoB;
-      bool later_a = false;
-      for (uint32_t j = s + 1; j < r1; ++j) {
-        const uint32_t rj = (uint32_t)L.skr[j] >> 12;
-        later_a |= (rj & ROLE_A) != 0;
-        if (rj & ROLE_B) {
-          if (nb == kNoB) nb = (uint16_t)j;
-          if (later_a || !(role & ROLE_A)) break;
+    // ---- per sorted position: next B and next A of its key run, as two
+    // segmented suffix-min scans over the window (O(log) steps, not a walk
+    // of the run per position); then first / last B and last A per key.
+    // Thread t holds positions 4 (NT - 1 - t) .. + 3, so the suffix scan over
+    // positions is a prefix scan over lanes (DPP) and waves (LDS).
+    {
+      constexpr uint32_t kInf = kNoB, kCut = 0x10000u;
+      const uint32_t pb = (uint32_t)(NT - 1 - tid) * PER;
+      uint32_t kq[PER + 1], rq[PER];
+#pragma unroll
+      for (int i = 0; i <= PER; ++i) {
+        const uint32_t q = pb + i;
+        const uint32_t kr = q < nw ? (uint32_t)L.skr[q] : 0xffffu;
+        kq[i] = q < nw ? (kr & 0xfffu) : 0xffffffffu - (uint32_t)i;   // past the window: all distinct
+        if (i < PER) rq[i] = q < nw ? kr >> 12 : 0u;
+      }
+      const uint32_t kprev = (pb > 0 && pb - 1 < nw) ? ((uint32_t)L.skr[pb - 1] & 0xfffu) : 0xfffffff0u;
+      uint32_t vb[PER], va[PER];
+      bool st[PER + 1];   // run start at position pb + i
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const uint32_t q = pb + i;
+        vb[i] = (q < nw && (rq[i] & ROLE_B)) ? q : kInf;
+        va[i] = (q < nw && (rq[i] & ROLE_A)) ? q : kInf;
+        st[i] = q >= nw || kq[i] != (i == 0 ? kprev : kq[i - 1]);
+      }
+      st[PER] = pb + PER >= nw || kq[PER] != kq[PER - 1];
+      // the thread's element: (cut, min from its first position to the first
+      // run start after it)
+      uint32_t lb = vb[0], la = va[0];
+      bool cut = false;
+#pragma unroll
+      for (int i = 1; i < PER; ++i) {
+        cut = cut || st[i];
+        if (!cut) {
+          lb = min(lb, vb[i]);
+          la = min(la, va[i]);
         }
       }
-      L.nextb[s] = nb;
-      if ((role & ROLE_A) && !later_a) {
-        L.klast[k] = L.sts[s];
-        L.khasa[k] = 1;
+      cut = cut || st[PER];
+      // combine(earlier = positions further right, own)
+      auto comb = [](uint32_t e, uint32_t o) -> uint32_t {
+        return ((e | o) & kCut) | ((o & kCut) ? (o & 0xffffu) : min(e & 0xffffu, o & 0xffffu));
+      };
+      auto scan = [&](uint32_t x) -> uint32_t {
+        constexpr int ident = (int)kInf;
+        x = comb((uint32_t)__builtin_amdgcn_update_dpp(ident, (int)x, 0x111, 0xf, 0xf, false), x);   // row_shr:1
+        x = comb((uint32_t)__builtin_amdgcn_update_dpp(ident, (int)x, 0x112, 0xf, 0xf, false), x);   // row_shr:2
+        x = comb((uint32_t)__builtin_amdgcn_update_dpp(ident, (int)x, 0x114, 0xf, 0xf, false), x);   // row_shr:4
+        x = comb((uint32_t)__builtin_amdgcn_update_dpp(ident, (int)x, 0x118, 0xf, 0xf, false), x);   // row_shr:8
+        x = comb((uint32_t)__builtin_amdgcn_update_dpp(ident, (int)x, 0x142, 0xa, 0xf, false), x);   // row_bcast:15
+        x = comb((uint32_t)__builtin_amdgcn_update_dpp(ident, (int)x, 0x143, 0xc, 0xf, false), x);   // row_bcast:31
+        return x;
+      };
+      const uint32_t ib = scan((cut ? kCut : 0u) | lb), ia = scan((cut ? kCut : 0u) | la);
+      const int lane = tid & 63, wv = tid >> 6;
+      if (lane == 63) {
+        L.scratch[wv] = ib;
+        L.scratch2[wv] = ia;
       }
-      if ((role & ROLE_B) && nb == kNoB) L.klb[k] = (uint16_t)s;
-      if (s == L.kstart[kbuf][k]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)s : nb;
+      lds_barrier();
+      uint32_t cb = kInf, ca = kInf;   // the waves to the right
+      for (int w = 0; w < wv; ++w) {
+        cb = comb(cb, L.scratch[w]);
+        ca = comb(ca, L.scratch2[w]);
+      }
+      const uint32_t pbv = (uint32_t)__shfl_up((int)ib, 1, 64), pav = (uint32_t)__shfl_up((int)ia, 1, 64);
+      const uint32_t xb = lane == 0 ? cb : comb(cb, pbv), xa = lane == 0 ? ca : comb(ca, pav);
+      // this thread's positions, right to left: next B / A of p_i is the
+      // suffix min at p_{i+1} unless p_{i+1} starts a run
+      uint32_t nbn = st[PER] ? kInf : (xb & 0xffffu), nan_ = st[PER] ? kInf : (xa & 0xffffu);
+#pragma unroll
+      for (int i = PER - 1; i >= 0; --i) {
+        const uint32_t q = pb + i;
+        const uint32_t nbi = nbn, nai = nan_;
+        const uint32_t sbi = min(vb[i], nbi), sai = min(va[i], nai);
+        nbn = st[i] ? kInf : sbi;
+        nan_ = st[i] ? kInf : sai;
+        if (q >= nw) continue;
+        const uint32_t k = kq[i], role = rq[i];
+        L.nextb[q] = (uint16_t)nbi;
+        if ((role & ROLE_A) && nai == kInf) {
+          L.klast[k] = L.sts[q];
+          L.khasa[k] = 1;
+        }
+        if ((role & ROLE_B) && nbi == kInf) L.klb[k] = (uint16_t)q;
+        if (st[i]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)q : (uint16_t)nbi;
+      }
     }
     if (cn > 0) {
       auto put_pc = [&](int j, uint64_t t, uint64_t x0, uint64_t x1) {
@@ -934,8 +997,21 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (2 + u < n) put_pc(2 + u, pv0[u], pv1[u], pv2[u]);
-      for (int j = 4; j < ni; ++j)   // long lists (rare)
-        put_pc(j, sl_ld(j, 0), c1 ? sl_ld(j, 2) : 0ull, c2 ? sl_ld(j, 3) : 0ull);
+      // longer lists (a few per wave): four slots' loads in flight at a time,
+      // not one dependent round trip per slot
+      for (int j0 = 4; j0 < ni; j0 += 4) {
+        uint64_t t[4], x0[4], x1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool ok = j0 + u < ni;
+          t[u] = ok ? sl_ld(j0 + u, 0) : 0ull;
+          x0[u] = (ok && c1) ? sl_ld(j0 + u, 2) : 0ull;
+          x1[u] = (ok && c2) ? sl_ld(j0 + u, 3) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (j0 + u < ni) put_pc(j0 + u, t[u], x0[u], x1[u]);
+      }
     }
     lds_barrier();
     // ---- key lanes: carried partials completed by the run's first B
