@@ -72,8 +72,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity check")
     ap.add_argument("--exchange", choices=["padded", "twophase"], default="padded",
-                    help="key shuffle of pattern records: fixed owner segments with in-band counts (no host "
-                         "round trip per step) or counts first, then an exact alltoallv")
+                    help="key shuffle (pattern records / config-5 rows): fixed owner segments with in-band "
+                         "counts (no host round trip per step) or counts first, then an exact alltoallv")
     ap.add_argument("--ingest", choices=["shuffle", "prepartitioned", "host", "host-pageable"],
                     default="shuffle",
                     help="multi-GPU pattern input: engine key shuffle over RCCL, or keyed upstream; "
@@ -486,12 +486,12 @@ def main():
             j = i % 2
             segs = rt.route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
                                    seq0=d["first"], seg_cap=cap, streams=d["stream"],
-                                   out=bufs.get(("psend", j)))
+                                   out=bufs.get(("psend", j)), rows=not pattern)
             bufs[("psend", j)] = segs
             torch.cuda.current_stream().wait_stream(guard[j])   # the walk that last read precv[j]
             recv = shuffle.exchange_padded(segs, world, out=bufs.get(("precv", j)))
             bufs[("precv", j)] = recv
-            rt.send_padded(recv, world, cap, n, signal=False)
+            rt.send_padded(recv, world, cap, n, signal=False, rows=not pattern)
             rt.signal(guard[j])
         rt.flush()
 
@@ -502,7 +502,7 @@ def main():
         from flink_siddhi import shuffle
         if not blist:
             return
-        if pattern and args.exchange == "padded" and seg_cap[0] == 0:
+        if args.exchange == "padded" and seg_cap[0] == 0:
             # calibrate the segment capacity on the first warm-up step
             # (two-phase: host counts), then every later step is padded
             recs, counts = route(blist[0], 0)
@@ -515,7 +515,7 @@ def main():
             if not blist:
                 rt.flush()
                 return
-        if pattern and args.exchange == "padded":
+        if args.exchange == "padded":
             run_padded(blist)
             return
         cur = route(blist[0], 0)
@@ -667,8 +667,11 @@ def main():
                         "keys": args.keys, "keys_dist": args.keys_dist if args.keys_dist == "uniform" else "zipf(s=1.1)",
                         "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
                         "parallelism": "key-sharded x%d" % world,
-                        "ingest": (("%s all-to-all row shuffle" % ("rccl" if _coll_device() == "cuda"
-                                                                   else "gloo host-staged"))
+                        "ingest": (("%s all-to-all row shuffle (%s)" % ("rccl" if _coll_device() == "cuda"
+                                                                        else "gloo host-staged",
+                                                                        "padded segments, in-band counts"
+                                                                        if args.exchange == "padded"
+                                                                        else "two-phase"))
                                    if shuffle_mode else "pre-partitioned (keyed upstream)")
                         if world > 1 else "local"}
                        if config5 else

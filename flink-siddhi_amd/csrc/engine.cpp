@@ -3233,7 +3233,7 @@ int cep_send_records_padded(cep_app* a, const void* segs, int world, int64_t seg
   // the headers' counts / error bits -> this engine's error word (reported
   // by the next flush); the null records flow through the partitions, which
   // skip role-0 records, so no count is read back here
-  launch_route_check((const uint64_t*)segs, world, seg_cap, wrw, (unsigned int*)a->err.p, a->stream);
+  launch_route_check((const uint64_t*)segs, world, seg_cap, wrw, 0, (unsigned int*)a->err.p, a->stream);
   RowsArgs rows{};
   rows.n = (int64_t)world * (1 + seg_cap);
   rows.row0 = 0;
@@ -3251,18 +3251,26 @@ int cep_row_words(cep_app* a) {
   return 3 + (int)a->app.inputs[layout].attrs.size();
 }
 
-int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out, int64_t rec_cap,
-                   int64_t* counts_host) {
-  if (!a || !b || !counts_host || world <= 0) return CEP_E_ARG;
+// seg_cap == 0: owner-contiguous rows, counts read back (cep_route_rows);
+// seg_cap > 0: padded owner segments, counts in-band (cep_route_rows_padded).
+static int route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out, int64_t rec_cap,
+                      int64_t* counts_host, int64_t seg_cap) {
+  if (!a || !b || world <= 0 || seg_cap < 0 || (seg_cap == 0 && !counts_host)) return CEP_E_ARG;
   if (world > kMaxWorld) return fail(a, CEP_E_ARG, "world exceeds " + std::to_string(kMaxWorld));
   int32_t kc[8];
   int layout;
   int rc = row_route_plan(a, kc, &layout);
   if (rc) return rc;
-  for (int d = 0; d < world; ++d) counts_host[d] = 0;
-  if (b->n == 0) return CEP_OK;
-  if (!rec_out || rec_cap < b->n)
-    return fail(a, CEP_E_ARG, "rec_out must hold at least n rows (" + std::to_string(b->n) + ")");
+  if (seg_cap == 0) {
+    for (int d = 0; d < world; ++d) counts_host[d] = 0;
+    if (b->n == 0) return CEP_OK;
+    if (!rec_out || rec_cap < b->n)
+      return fail(a, CEP_E_ARG, "rec_out must hold at least n rows (" + std::to_string(b->n) + ")");
+  } else {
+    if (b->n == 0) return fail(a, CEP_E_ARG, "padded row shuffle needs a non-empty batch");
+    if (!rec_out || rec_cap < (int64_t)world * (1 + seg_cap))
+      return fail(a, CEP_E_ARG, "seg_out must hold world * (1 + seg_cap) rows");
+  }
   if (b->stream) {
     // a multi-stream batch needs one layout for all its streams (batch_rows)
   } else if (kc[b->input] != -2) {
@@ -3296,12 +3304,18 @@ int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void
   ra.arena = (uint64_t*)a->route_arena.p;
   ra.tcount = (uint32_t*)a->route_tcount.p;
   ra.err = (unsigned int*)a->rerr.p;
+  ra.seg_cap = seg_cap;
   {
     LaunchTimer t(a, CEP_K_ROUTE, rs);
     launch_route_rows(ra, ntiles, (uint32_t*)a->route_toffs.p, (unsigned long long*)a->route_dcount.p,
                       (uint64_t*)rec_out, rs);
   }
   if (slot >= 0) hipEventRecord(a->hs[slot].free, rs);
+  if (seg_cap > 0) {   // nothing read back: the error bits travel in the headers
+    hipMemsetAsync(a->rerr.p, 0, 64, rs);
+    a->batches++;
+    return hipGetLastError() == hipSuccess ? CEP_OK : fail(a, CEP_E_DEVICE, "padded row route launch failed");
+  }
   std::vector<unsigned long long> dc(world);
   unsigned int re = 0;
   hipMemcpyAsync(dc.data(), a->route_dcount.p, world * 8, hipMemcpyDeviceToHost, rs);
@@ -3320,6 +3334,28 @@ int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void
   }
   a->batches++;
   return CEP_OK;
+}
+
+int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out, int64_t rec_cap,
+                   int64_t* counts_host) {
+  return route_rows(a, b, world, seq0, rec_out, rec_cap, counts_host, 0);
+}
+
+int cep_route_rows_padded(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* seg_out,
+                          int64_t seg_out_cap, int64_t seg_cap) {
+  if (seg_cap <= 0) return CEP_E_ARG;
+  return route_rows(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap);
+}
+
+int cep_send_rows_padded(cep_app* a, const void* segs, int world, int64_t seg_cap, int64_t events_represented) {
+  if (!a || !segs || world <= 0 || world > kMaxWorld || seg_cap <= 0) return CEP_E_ARG;
+  if (!a->enabled) return CEP_OK;
+  const int w = cep_row_words(a);
+  if (w < 0) return -w;
+  // headers -> this engine's error word; header and null rows carry stream
+  // handle kRowNullStream, which no query reads
+  launch_route_check((const uint64_t*)segs, world, seg_cap, w, 1, (unsigned int*)a->err.p, a->stream);
+  return cep_send_rows(a, segs, (int64_t)world * (1 + seg_cap), events_represented);
 }
 
 int cep_send_rows(cep_app* a, const void* recs, int64_t n, int64_t events_represented) {

@@ -183,7 +183,12 @@ struct RowRouteArgs {
   uint64_t* arena;             // [ntiles][tile_rows * wrw], owner-grouped per tile
   uint32_t* tcount;            // [ntiles][world]
   unsigned int* err;
+  int64_t seg_cap;             // > 0: padded owner segments (cep_route_rows_padded)
 };
+
+// Stream handle of the padded row shuffle's header and null rows: no input
+// handle is ever this large (<= 8 streams), so no query reads them.
+constexpr uint32_t kRowNullStream = 31;
 
 struct RowUnpackArgs {
   const uint64_t* recs;
@@ -210,6 +215,7 @@ struct RouteArgs {
   // > 0: padded segments (cep_route_batch_padded): owner d's records go to
   // out + (d * (1 + seg_cap) + 1) * wrw, at most seg_cap of them
   int64_t seg_cap;
+  int32_t row_mode;            // padded segments of whole rows (cep_route_rows_padded)
 };
 
 struct WalkArgs {
@@ -574,7 +580,7 @@ void launch_route_collect(const RouteArgs& a, int64_t ntiles, uint32_t* toffs,
                           unsigned long long* dcount, uint64_t* out, hipStream_t s);
 // padded key shuffle: segment headers + null tails (sender), header check (owner)
 void launch_route_pad(const RouteArgs& a, const unsigned long long* dcount, uint64_t* out, hipStream_t s);
-void launch_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, unsigned int* err,
+void launch_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, int row_mode, unsigned int* err,
                         hipStream_t s);
 void launch_route_rows(const RowRouteArgs& a, int64_t ntiles, uint32_t* toffs,
                        unsigned long long* dcount, uint64_t* out, hipStream_t s);

@@ -857,12 +857,18 @@ void launch_route_rows(const RowRouteArgs& a, int64_t ntiles, uint32_t* toffs,
                        unsigned long long* dcount, uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_route_rows, dim3((unsigned)ntiles), dim3(kPartThreads), 0, s, a);
   RouteArgs ra{};
+  ra.rows = a.rows;
   ra.world = a.world;
   ra.wrw = a.wrw;
   ra.tile_rows = a.tile_rows;
+  ra.seq0 = a.seq0;
   ra.arena = a.arena;
   ra.tcount = a.tcount;
+  ra.err = a.err;
+  ra.seg_cap = a.seg_cap;
+  ra.row_mode = 1;
   launch_route_collect(ra, ntiles, toffs, dcount, out, s);
+  if (a.seg_cap > 0) launch_route_pad(ra, dcount, out, s);
 }
 
 void launch_unpack_rows(const RowUnpackArgs& a, hipStream_t s) {
@@ -932,11 +938,13 @@ __global__ __launch_bounds__(256) void k_route_pad(RouteArgs a, const unsigned l
   const int64_t used = (int64_t)cnt < a.seg_cap ? (int64_t)cnt : a.seg_cap;
   const int64_t r0 = a.rows.row0, r1 = a.rows.row0 + a.rows.n - 1;
   uint64_t* seg = out + (int64_t)d * (1 + a.seg_cap) * wrw;
+  const uint64_t ovf = (int64_t)cnt > a.seg_cap ? 1ull << 63 : 0ull;
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)wrw) {
     const unsigned int e = *(volatile unsigned int*)a.err;
     uint64_t h = 0;
-    if (threadIdx.x == 0)
-      h = (cnt & 0xffffffffull) | ((uint64_t)(e & 0xffffu) << 40) | ((int64_t)cnt > a.seg_cap ? 1ull << 63 : 0ull);
+    if (threadIdx.x == 0)   // records: count | errors << 40 (role 0); rows: null stream | errors << 8 | count << 32
+      h = a.row_mode ? (uint64_t)kRowNullStream | ((uint64_t)(e & 0xffffffu) << 8) | ((cnt & 0x7fffffffull) << 32) | ovf
+                     : (cnt & 0xffffffffull) | ((uint64_t)(e & 0xffffu) << 40) | ovf;
     else if (threadIdx.x == 1)
       h = (uint64_t)a.seq0;
     else if (threadIdx.x == 2)
@@ -948,17 +956,18 @@ __global__ __launch_bounds__(256) void k_route_pad(RouteArgs a, const unsigned l
   uint64_t* tail = seg + (1 + used) * wrw;
   for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nul; w += (int64_t)gridDim.x * blockDim.x) {
     const int f = (int)(w % wrw);
-    tail[w] = f == 1 ? tseq : (f == 2 ? tts : 0ull);
+    tail[w] = f == 1 ? tseq : (f == 2 ? tts : (f == 0 && a.row_mode ? (uint64_t)kRowNullStream : 0ull));
   }
 }
 
 // Owner side: a flagged header (overflowed segment or a sender-side route
 // error) becomes the owner's error word, reported by its next flush.
-__global__ void k_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, unsigned int* err) {
+__global__ void k_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, int row_mode,
+                              unsigned int* err) {
   const int d = threadIdx.x;
   if (d >= world) return;
   const uint64_t h = segs[(int64_t)d * (1 + seg_cap) * wrw];
-  unsigned int e = (unsigned int)((h >> 40) & 0xffffu);
+  unsigned int e = row_mode ? (unsigned int)((h >> 8) & 0xffffffu) : (unsigned int)((h >> 40) & 0xffffu);
   if (h >> 63) e |= ERR_SHUFFLE_CAP;
   if (e) atomicOr(err, e);
 }
@@ -969,9 +978,9 @@ void launch_route_pad(const RouteArgs& a, const unsigned long long* dcount, uint
   hipLaunchKernelGGL(k_route_pad, dim3(bx, (unsigned)a.world), dim3(256), 0, s, a, dcount, out);
 }
 
-void launch_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, unsigned int* err,
+void launch_route_check(const uint64_t* segs, int world, int64_t seg_cap, int wrw, int row_mode, unsigned int* err,
                         hipStream_t s) {
-  hipLaunchKernelGGL(k_route_check, dim3(1), dim3(64), 0, s, segs, world, seg_cap, wrw, err);
+  hipLaunchKernelGGL(k_route_check, dim3(1), dim3(64), 0, s, segs, world, seg_cap, wrw, row_mode, err);
 }
 
 void launch_route(const RouteArgs& a, int64_t ntiles, bool vm, uint32_t* toffs,

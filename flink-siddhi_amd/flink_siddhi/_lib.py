@@ -163,6 +163,9 @@ SIGNATURES = {
                                          C.c_void_p, C.c_int64, C.c_int64]),
     "cep_send_records_padded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_int64]),
     "cep_route_signal": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "cep_route_rows_padded": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
+                                        C.c_void_p, C.c_int64, C.c_int64]),
+    "cep_send_rows_padded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_int64]),
     "cep_row_words": (C.c_int, [C.c_void_p]),
     "cep_route_rows": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
                                  C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),

@@ -293,11 +293,12 @@ class SiddhiAppRuntime:
         return out, [int(c) for c in counts]
 
     def route_padded(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int, seg_cap: int,
-                     streams=None, out=None, wait: bool = True):
-        """Padded sender side (cep_route_batch_padded): a uint64 device tensor
-        [world * (1 + seg_cap), record_words] of fixed owner segments with the
-        counts in-band (segment headers).  Nothing is read back: the route is
-        only queued, so the step needs no host round trip."""
+                     streams=None, out=None, wait: bool = True, rows: bool = False):
+        """Padded sender side (cep_route_batch_padded; rows=True:
+        cep_route_rows_padded): a uint64 device tensor [world * (1 + seg_cap),
+        words] of fixed owner segments with the counts in-band (segment
+        headers).  Nothing is read back: the route is only queued, so the step
+        needs no host round trip."""
         import torch
         h = self.input_handle(stream_id)
         defs = self.stream_definition(stream_id)
@@ -313,31 +314,32 @@ class SiddhiAppRuntime:
         if streams is not None:
             sp, k = _ptr(streams, np.dtype("uint8"), True)
             keep.append(k)
-        rows = world * (1 + int(seg_cap))
-        w = self.record_words()
-        if out is None or out.shape[0] < rows or out.shape[1] != w:
-            out = torch.empty((rows, w), dtype=torch.int64, device=ts.device)
+        nrows = world * (1 + int(seg_cap))
+        w = self.row_words() if rows else self.record_words()
+        if out is None or out.shape[0] < nrows or out.shape[1] != w:
+            out = torch.empty((nrows, w), dtype=torch.int64, device=ts.device)
         b = L.cep_batch(n=_len(ts), ts=C.c_void_p(ts.data_ptr()), stream=sp, input=h, ncols=len(cols),
                         cols=ptrs, on_device=1)
         if wait:
             self._wait_producer(ts)
-        self._check(self._lib.cep_route_batch_padded(self._h, C.byref(b), world, seq0,
-                                                     C.c_void_p(out.data_ptr()), out.shape[0], int(seg_cap)))
+        fn = self._lib.cep_route_rows_padded if rows else self._lib.cep_route_batch_padded
+        self._check(fn(self._h, C.byref(b), world, seq0, C.c_void_p(out.data_ptr()), out.shape[0], int(seg_cap)))
         # torch's stream (the all-to-all) must not read the segments before the
         # route stream wrote them; the walk queued on the engine stream is not
         # waited for
         s = torch.cuda.current_stream(ts.device).cuda_stream
         self._check(self._lib.cep_route_signal(self._h, C.c_void_p(s)))
-        return out[:rows]
+        return out[:nrows]
 
     def send_padded(self, segs, world: int, seg_cap: int, events_represented: int = 0,
-                    signal: bool = True):
+                    signal: bool = True, rows: bool = False):
         """Owner side of the padded shuffle: the world received segments in
-        source-rank order.  An overflowed segment fails the next flush."""
+        source-rank order (rows=True: whole rows of the row shuffle).  An
+        overflowed segment fails the next flush."""
         if getattr(segs, "is_cuda", False):
             self._wait_producer(segs)
-        self._check(self._lib.cep_send_records_padded(self._h, C.c_void_p(segs.data_ptr()), world,
-                                                      int(seg_cap), events_represented))
+        fn = self._lib.cep_send_rows_padded if rows else self._lib.cep_send_records_padded
+        self._check(fn(self._h, C.c_void_p(segs.data_ptr()), world, int(seg_cap), events_represented))
         if signal and getattr(segs, "is_cuda", False):
             self._signal_consumer(segs)
 

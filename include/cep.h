@@ -324,6 +324,16 @@ int cep_row_words(cep_app* app);   /* < 0: -status */
 int cep_route_rows(cep_app* app, const cep_batch* batch, int world, int64_t seq0, void* rec_out,
                    int64_t rec_cap, int64_t* counts_host);
 int cep_send_rows(cep_app* app, const void* recs, int64_t n, int64_t events_represented);
+/* Padded row shuffle: as cep_route_batch_padded, for whole rows.  Header and
+ * null rows carry stream handle 31 (no input has it, so no query reads them):
+ * header word 0 = 31 | route error bits << 8 | count << 32 | 1 << 63 on
+ * overflow, words 1 / 2 = seq / ts of the batch's first row; null rows the
+ * seq / ts of its last.  cep_send_rows_padded checks the headers on the
+ * device and feeds the world segments (source-rank order) as one batch. */
+int cep_route_rows_padded(cep_app* app, const cep_batch* batch, int world, int64_t seq0, void* seg_out,
+                          int64_t seg_out_cap, int64_t seg_cap);
+int cep_send_rows_padded(cep_app* app, const void* segs, int world, int64_t seg_cap,
+                         int64_t events_represented);
 
 /* ---- dynamic plans (control events) ---------------------------------------
  * One operator hosting many plans, as AbstractSiddhiOperator keeps one

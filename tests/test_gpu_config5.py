@@ -143,8 +143,8 @@ def test_config5_exact_predicates():
     assert sum(len(want.get(o, [])) for o in outs if o.startswith("Seq")) > 0
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_config5_row_shuffle_matches_oracle(world):
+@pytest.mark.parametrize("world,padded", [(2, False), (3, False), (2, True), (3, True)])
+def test_config5_row_shuffle_matches_oracle(world, padded):
     # config 5 across GPUs (simulated worlds on one GPU): each source slice is
     # routed whole-row by cep_route_rows (no push-down: sequences need every
     # row), owner r receives the slices' r-segments in source order and runs
@@ -165,6 +165,7 @@ def test_config5_row_shuffle_matches_oracle(world):
         for out in outputs():
             o.add_callback(out)
     m = n // (2 * world)
+    cap = m // world + m // (2 * world) + 64   # padded: ample for 48 keys
     for step in range(2):   # two shuffle steps: state carries across them
         segs = [[] for _ in range(world)]
         for src in range(world):
@@ -173,6 +174,13 @@ def test_config5_row_shuffle_matches_oracle(world):
             e = s + m
             d = {c: torch.from_numpy(np.ascontiguousarray(w[c][s:e])).cuda()
                  for c in ("k", "ts", "id", "price", "stream")}
+            if padded:   # cep_route_rows_padded: fixed segments, counts in-band
+                rows = sender.route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
+                                           seq0=int(s), seg_cap=cap, streams=d["stream"], rows=True)
+                torch.cuda.synchronize()
+                for r in range(world):
+                    segs[r].append(rows[r * (1 + cap):(r + 1) * (1 + cap)].clone())
+                continue
             rows, counts = sender.route_rows("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
                                              world, seq0=int(s), streams=d["stream"])
             off = np.concatenate([[0], np.cumsum(counts)])
@@ -180,7 +188,10 @@ def test_config5_row_shuffle_matches_oracle(world):
                 segs[r].append(rows[off[r]:off[r + 1]].clone())
         for r in range(world):
             recv = torch.cat(segs[r], dim=0)
-            owners[r].send_rows(recv, recv.shape[0], 0)
+            if padded:
+                owners[r].send_padded(recv, world, cap, 0, rows=True)
+            else:
+                owners[r].send_rows(recv, recv.shape[0], 0)
     got = {o: [] for o in outputs()}
     for r in range(world):
         owners[r].flush()
