@@ -140,3 +140,31 @@ def test_count_group_survives_world_reinit():
         assert not isinstance(res[r], str), res[r]
         for it in range(2):
             assert res[r][it] == [s * 10 + r + it for s in range(world)]
+
+
+def _calib_main(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # every rank learns the largest per-owner count of any rank
+        counts = [100 * (rank + 1) + d for d in range(world)]
+        q.put((rank, shuffle.calibrated_capacity(counts, slack=0.5, floor=7)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_calibrated_capacity_is_the_global_max_plus_slack():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calib_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    top = 100 * world + world - 1
+    assert all(v == int(top + top * 0.5) + 7 for v in res.values()), res
