@@ -517,14 +517,14 @@ struct CfWalkLds {
     uint64_t kent[WIN];                // seq << 20 | key << 11 | slot, grouped by key
     uint64_t scap[NW > 0 ? NW : 1][WIN];   // sorted: physical carried words
   };
-  union {
+  union alignas(16) {
     uint16_t sorted[WIN];              // window slot per sorted position
     uint16_t nextb[WIN];               // sorted position of the run's next B, or kNoB
   };
-  uint32_t sts[WIN];                   // sorted: ts - chunk ts base
+  alignas(16) uint32_t sts[WIN];       // sorted: ts - chunk ts base
   uint32_t sseq[WIN];                  // sorted: chunk-relative row (arrival order)
-  uint16_t skr[WIN];                   // sorted: key in bucket | role << 12
-  uint16_t v[WIN];                     // output row offset per sorted position
+  alignas(16) uint16_t skr[WIN];       // sorted: key in bucket | role << 12
+  alignas(16) uint16_t v[WIN];         // output row offset per sorted position
   uint16_t kfb[kCfMaxKeys];            // first B of the key's run, or kNoB
   uint16_t klb[kCfMaxKeys];            // last B of the key's run, or kNoB
   uint8_t khasa[kCfMaxKeys];
@@ -906,11 +906,19 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     {
       constexpr uint32_t kInf = kNoB, kCut = 0x10000u;
       const uint32_t pb = (uint32_t)(NT - 1 - tid) * PER;
-      uint32_t kq[PER + 1], rq[PER];
+      uint32_t kq[PER + 1], rq[PER], krw[PER + 1];
+      if constexpr (PER == 4) {   // one 8-byte read (lane-consecutive) + the next thread's first
+        const uint2 k2 = *(const uint2*)&L.skr[pb];
+        krw[0] = k2.x & 0xffffu; krw[1] = k2.x >> 16; krw[2] = k2.y & 0xffffu; krw[3] = k2.y >> 16;
+        krw[4] = pb + 4 < nw ? (uint32_t)L.skr[pb + 4] : 0xffffu;
+      } else {
+#pragma unroll
+        for (int i = 0; i <= PER; ++i) krw[i] = pb + i < nw ? (uint32_t)L.skr[pb + i] : 0xffffu;
+      }
 #pragma unroll
       for (int i = 0; i <= PER; ++i) {
         const uint32_t q = pb + i;
-        const uint32_t kr = q < nw ? (uint32_t)L.skr[q] : 0xffffu;
+        const uint32_t kr = krw[i];
         kq[i] = q < nw ? (kr & 0xfffu) : 0xffffffffu - (uint32_t)i;   // past the window: all distinct
         if (i < PER) rq[i] = q < nw ? kr >> 12 : 0u;
       }
@@ -969,6 +977,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       // this thread's positions, right to left: next B / A of p_i is the
       // suffix min at p_{i+1} unless p_{i+1} starts a run
       uint32_t nbn = st[PER] ? kInf : (xb & 0xffffu), nan_ = st[PER] ? kInf : (xa & 0xffffu);
+      uint32_t nbo[PER];
 #pragma unroll
       for (int i = PER - 1; i >= 0; --i) {
         const uint32_t q = pb + i;
@@ -976,9 +985,10 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         const uint32_t sbi = min(vb[i], nbi), sai = min(va[i], nai);
         nbn = st[i] ? kInf : sbi;
         nan_ = st[i] ? kInf : sai;
+        nbo[i] = nbi;
         if (q >= nw) continue;
         const uint32_t k = kq[i], role = rq[i];
-        L.nextb[q] = (uint16_t)nbi;
+        if constexpr (PER != 4) L.nextb[q] = (uint16_t)nbi;
         if ((role & ROLE_A) && nai == kInf) {
           L.klast[k] = L.sts[q];
           L.khasa[k] = 1;
@@ -986,6 +996,8 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         if ((role & ROLE_B) && nbi == kInf) L.klb[k] = (uint16_t)q;
         if (st[i]) L.kfb[k] = (role & ROLE_B) ? (uint16_t)q : (uint16_t)nbi;
       }
+      if constexpr (PER == 4)   // positions past the window get kNoB, never read
+        *(uint2*)&L.nextb[pb] = make_uint2((nbo[0] & 0xffffu) | (nbo[1] << 16), (nbo[2] & 0xffffu) | (nbo[3] << 16));
     }
     if (cn > 0) {
       auto put_pc = [&](int j, uint64_t t, uint64_t x0, uint64_t x1) {
@@ -1058,16 +1070,35 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     {
       uint32_t vals[PER];
       uint32_t sum = 0;
+      // a thread's PER contiguous positions: one wide LDS read per array
+      // (lane-consecutive, no bank conflicts) where PER is 4
+      uint32_t krv[PER], nbv[PER], stv[PER];
+      if constexpr (PER == 4) {
+        const uint2 k2 = *(const uint2*)&L.skr[tid * 4];
+        const uint2 n2 = *(const uint2*)&L.nextb[tid * 4];
+        const uint4 t4 = *(const uint4*)&L.sts[tid * 4];
+        krv[0] = k2.x & 0xffffu; krv[1 % PER] = k2.x >> 16; krv[2 % PER] = k2.y & 0xffffu; krv[3 % PER] = k2.y >> 16;
+        nbv[0] = n2.x & 0xffffu; nbv[1 % PER] = n2.x >> 16; nbv[2 % PER] = n2.y & 0xffffu; nbv[3 % PER] = n2.y >> 16;
+        stv[0] = t4.x; stv[1 % PER] = t4.y; stv[2 % PER] = t4.z; stv[3 % PER] = t4.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+          const uint32_t q = tid * PER + i;
+          krv[i] = q < nw ? L.skr[q] : 0u;
+          nbv[i] = q < nw ? L.nextb[q] : kNoB;
+          stv[i] = q < nw ? L.sts[q] : 0u;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const uint32_t q = tid * PER + i;
         uint32_t val = 0;
         if (q < nw) {
-          const uint32_t kr = L.skr[q];
+          const uint32_t kr = krv[i];
           const uint32_t k = kr & 0xfffu;
-          const uint16_t nb = L.nextb[q];
+          const uint32_t nb = nbv[i];
           if (((kr >> 12) & ROLE_A) && nb != kNoB) {
-            const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
+            const int64_t d = (int64_t)L.sts[nb] - (int64_t)stv[i];
             val = (W < 0 || (d < 0 ? -d : d) <= W) ? (1u << 20) | 1u : 0u;
           }
           if (q == L.kstart[kbuf][k]) val += L.cm[k];
@@ -1077,12 +1108,20 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       }
       uint32_t total;
       uint32_t off = bscan<NT, false>(sum, L.scratch2, &total);
+      uint32_t vv[PER];
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const uint32_t q = tid * PER + i;
-        L.v[q] = (uint16_t)(off & 0xfffffu);
+        vv[i] = off & 0xfffffu;
         if ((vals[i] >> 20) && (off >> 20) < (uint32_t)kCfOmap) omap[off >> 20] = (uint16_t)q;
         off += vals[i];
+      }
+      if constexpr (PER == 4) {
+        *(uint2*)&L.v[tid * 4] = make_uint2((vv[0] & 0xffffu) | (vv[1 % PER] << 16),
+                                            (vv[2 % PER] & 0xffffu) | (vv[3 % PER] << 16));
+      } else {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) L.v[tid * PER + i] = (uint16_t)vv[i];
       }
       const uint32_t rows = total & 0xfffffu;
       if (tid == 0) {
