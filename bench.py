@@ -684,7 +684,7 @@ def main():
             "roofline_kernels": per_kernel,
             "kernels": kern,
             "parity": parity,
-            "host_io": ({"ingest": args.ingest, "bytes_in_per_event": in_b,
+            "host_io": ({"ingest": args.ingest if host_ingest else "device-resident", "bytes_in_per_event": in_b,
                          "pcie_in_GBs": round(value * in_b / 1e9, 2) if host_ingest else 0.0,
                          "delivered_rows": delivered[0] - d0 if args.deliver else None,
                          "delivered_rows_per_s": round((delivered[0] - d0) / dt_max, 1) if args.deliver else None,
