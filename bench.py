@@ -92,12 +92,70 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nranks, argv=None, script=None, env=None, poll_s=0.2):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes of
+    this same command (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT in their environment) and wait for them.  The
+    parent never imports torch or touches the GPU, so nothing is exec'd from a
+    GPU-initialised process.  Rank 0 prints the JSON line on the inherited
+    stdout.  If any rank exits non-zero the others are terminated (by their
+    own PIDs) and the parent returns that rank's exit code.  Reference
+    parallelism: one Siddhi runtime per Flink subtask
+    (core/.../operator/AbstractSiddhiOperator.java:308-312), events routed by
+    router/DynamicPartitioner.java:43-60 / HashPartitioner.java:24-26."""
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    script = str(Path(__file__).resolve()) if script is None else script
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base["MASTER_PORT"] = base.get("MASTER_PORT") or str(_free_port())
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(nranks):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                 LOCAL_WORLD_SIZE=str(nranks), GROUP_RANK="0", CEP_LAUNCHED_BY="bench.py")
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print("bench.py launcher: rank %d exited with %d; stopping the other ranks"
+                          % (procs.index(p), c), file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def dist_init(args):
     """One process per GPU.  CEP_DIST_BACKEND=gloo (rehearsal on a box with
     fewer GPUs than ranks: ranks share devices, exchanges staged via host)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     import torch
     backend = os.environ.get("CEP_DIST_BACKEND", "nccl")
     if backend != "nccl":
@@ -113,12 +171,20 @@ def dist_init(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     return world, rank, local
 
 
 def _coll_device():
     import torch.distributed as dist
     return "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+
+def _backend_name(world):
+    if world == 1:
+        return None
+    import torch.distributed as dist
+    return str(dist.get_backend())
 
 
 def barrier(world):
@@ -363,6 +429,9 @@ def config5_parity(args, opts, n, steps):
 # ------------------------------------------------------------------- main --
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us: start the ranks ourselves (before any torch import)
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import flink_siddhi as fs
     from flink_siddhi import _lib as L
@@ -645,6 +714,9 @@ def main():
         out = {
             "metric": "matched-pattern events/sec (whole node) at 1/2/4/8 MI355X + % HBM roofline",
             "value": round(value, 1), "unit": "events/s", "n_gpus": world,
+            "backend": _backend_name(world),
+            "rccl_world": world if _backend_name(world) == "nccl" else 0,
+            "launcher": os.environ.get("CEP_LAUNCHED_BY", "torchrun" if world > 1 else "none"),
             "steps": steps, "warmup": warm, "ms_per_step": round(1e3 * dt_max / steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f64+int32+int64", "data": "synthetic (splitmix64 counter stream, BASELINE.md §3)",

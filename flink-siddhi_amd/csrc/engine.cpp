@@ -202,6 +202,7 @@ struct cep_app {
   // routing step s+1 overlaps the walk of step s (it touches no walk state)
   hipStream_t rstream = nullptr;
   hipEvent_t r_ready = nullptr;
+  hipEvent_t r_host = nullptr;     // a host batch's route (engine stream) joined into the route stream
   bool enabled = true;
   std::string last_error;
   std::vector<std::string> dict;
@@ -911,7 +912,8 @@ int create_runtime(cep_app* a) {
       hipEventCreateWithFlags(&a->out_ready, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&a->copy, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&a->rstream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&a->r_ready, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&a->r_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&a->r_host, hipEventDisableTiming) != hipSuccess)
     return fail(a, CEP_E_DEVICE, "hipStreamCreate failed");
   size_t cb = std::max<size_t>(app.code.size(), 1) * sizeof(Ins);
   size_t kb = std::max<size_t>(app.konst.size(), 1) * 8;
@@ -1511,10 +1513,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     }
     {
       LaunchTimer t(a, CEP_K_CF_WALK);
-      // k_cfwalk unless CEP_CF_WALK=2 selects the owner-wave walk (cf_walk.hip)
-      static const bool walk2 = std::getenv("CEP_CF_WALK") && std::atoi(std::getenv("CEP_CF_WALK")) == 2;
-      if (walk2) launch_cf_walk2(wa, P, a->stream);
-      else launch_cf_walk(wa, P, a->stream);
+      launch_cf_walk(wa, P, a->stream);
     }
     if (hot) {
       if (divert && !hot_serial) hipStreamWaitEvent(a->stream, rt.hot_join, 0);
@@ -2162,6 +2161,7 @@ void cep_destroy(cep_app* a) {
   if (a->ext_ready) hipEventDestroy(a->ext_ready);
   if (a->out_ready) hipEventDestroy(a->out_ready);
   if (a->r_ready) hipEventDestroy(a->r_ready);
+  if (a->r_host) hipEventDestroy(a->r_host);
   if (a->rstream) {
     hipStreamSynchronize(a->rstream);
     hipStreamDestroy(a->rstream);
@@ -2822,7 +2822,9 @@ int cep_restore(cep_app* a, const uint8_t* buf, size_t len) {
       !get(&ev, 8) || !get(&np, 4))
     return fail(a, CEP_E_STATE, "not a libcep snapshot");
   if (h != plan_hash(a->app) || np != a->pats.size())
-    return fail(a, CEP_E_STATE, "snapshot was taken with a different plan");
+    return fail(a, CEP_E_STATE, "snapshot was taken with a different plan (or a build that compiled it "
+                                "differently: 2-state patterns with s1-dependent conditions need CEP_PAIR_WALK=1 "
+                                "to restore snapshots of builds before round 4)");
   // Phase 1: parse and validate everything into host buffers; nothing on the
   // device changes until the whole snapshot is known to be good.
   struct PatState {
@@ -3141,10 +3143,21 @@ int cep_route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, voi
   return route_batch(a, b, world, seq0, rec_out, rec_cap, counts_host, 0);
 }
 
+// A host batch is staged and routed on the engine stream; join that into the
+// route stream so cep_route_signal (which records on the route stream) also
+// orders a consumer after it (the padded routes read nothing back).
+static int route_join_host(cep_app* a, const cep_batch* b, int rc) {
+  if (rc != CEP_OK || !b || b->on_device) return rc;
+  if (hipEventRecord(a->r_host, a->stream) != hipSuccess ||
+      hipStreamWaitEvent(a->rstream, a->r_host, 0) != hipSuccess)
+    return fail(a, CEP_E_DEVICE, "route: stream join failed");
+  return rc;
+}
+
 int cep_route_batch_padded(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* seg_out,
                            int64_t seg_out_cap, int64_t seg_cap) {
   if (seg_cap <= 0) return CEP_E_ARG;
-  return route_batch(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap);
+  return route_join_host(a, b, route_batch(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap));
 }
 
 // Row shuffle plan: per input handle the owner key column (-1: any owner,
@@ -3344,7 +3357,7 @@ int cep_route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void
 int cep_route_rows_padded(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* seg_out,
                           int64_t seg_out_cap, int64_t seg_cap) {
   if (seg_cap <= 0) return CEP_E_ARG;
-  return route_rows(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap);
+  return route_join_host(a, b, route_rows(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap));
 }
 
 int cep_send_rows_padded(cep_app* a, const void* segs, int world, int64_t seg_cap, int64_t events_represented) {

@@ -562,8 +562,6 @@ void launch_mq_partition(const MqPartArgs& a, hipStream_t s);
 void launch_mq_walk(const MqWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s);
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s);
-// owner-wave walk (cf_walk.hip): the default; CEP_CF_WALK=1 selects k_cfwalk
-void launch_cf_walk2(const CfWalkArgs& a, int nbuckets, hipStream_t s);
 void launch_keymap(const KeyMapArgs& a, hipStream_t s);
 void launch_route_keys(const RouteKeyArgs& a, hipStream_t s);
 void launch_hot_match(const HotArgs& a, hipStream_t s);

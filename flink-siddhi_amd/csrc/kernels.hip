@@ -1365,6 +1365,20 @@ __device__ uint32_t agg_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int k, i
 // either advances a partial (staying in a count state, or moving to a later
 // state skipping optional ones) or discards it.  Matches reserve output rows
 // one by one (a lane's rows of one event stay in creation order).
+// Reserve `need` slots of a pool without pushing its cursor past `cap`:
+// ~0 when they do not fit (a failed booking leaves the cursor as it was, so
+// smaller bookings later in the launch can still succeed).
+__device__ __forceinline__ unsigned long long pool_reserve(unsigned long long* cursor, unsigned long long need,
+                                                           unsigned long long cap) {
+  unsigned long long o = *(volatile unsigned long long*)cursor;
+  while (true) {
+    if (o + need > cap) return ~0ull;
+    const unsigned long long prev = atomicCAS(cursor, o, o + need);
+    if (prev == o) return o;
+    o = prev;
+  }
+}
+
 template <bool kVm>
 __device__ __forceinline__ bool nfa_cond(const WalkArgs& a, uint64_t* R, int j, uint32_t role,
                                          const uint64_t* slot, int64_t st, const uint64_t* rec, int64_t ts_base) {
@@ -1412,34 +1426,46 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
   int n = ovf0 ? (int)(ext0 & 0x7fffffffull) : (int)(hdr & 0xffu);
   bool started = ((hdr >> 8) & 1u) != 0;
   // Working storage.  Inline: list [0, S), staging [S, 2S), word stride ks.
-  // A list that may outgrow S in this window (n + its records > S: each
-  // record adds at most one partial) works in one pool run instead: list
-  // [0, M), staging [M, 2M), word stride 1; it is written back in the
-  // at-rest layout (inline [0, S) + tail run) when the key is done.
+  // Each record adds at most one partial, so a list can outgrow S only once
+  // it holds S partials.  Then (lazily, before that record) the key moves to
+  // one pool run sized for the rest of the window: list [0, M), staging
+  // [M, 2M), word stride 1, M = n + records left; it is written back in the
+  // at-rest layout (inline [0, S) + tail run) when the key is done.  A key
+  // whose list stays within S books no pool slots at all.
   uint64_t* run = nullptr;
   unsigned long long roff = 0;
   int64_t st = ks;
   int CAP = S;
-  const int64_t M = (int64_t)n + (int64_t)(L.kstart[k + 1] - L.kstart[k]);
-  if (M > S && a.pool_wr) {
+  bool pool_failed = false;
+  auto grow = [&](uint32_t q_next) -> bool {
+    // false only when an overflowed key cannot get its run: it keeps its state
+    if (run || pool_failed || !a.pool_wr) return true;
+    const int64_t M = (int64_t)n + (int64_t)(L.kstart[k + 1] - q_next);
     const unsigned long long need = 2ull * (unsigned long long)M;
-    const unsigned long long o = atomicAdd(a.pool_cursor, need);
-    if (o + need > a.pool_cap) {
-      set_err(a.err, ERR_POOL);
-      if (ovf0) return;   // the key keeps its state; the error is reported
-    } else {
-      roff = o;
-      run = a.pool_wr + o * (uint64_t)sw;
-      st = 1;
-      CAP = (int)M;
-      const uint64_t* tail =
-          ovf0 ? (((ext0 >> 31) & 1ull) ? (const uint64_t*)a.pool_wr : a.pool_rd) + (ext0 >> 32) * (uint64_t)sw
-               : nullptr;
-      for (int j = 0; j < n; ++j)
-        for (int x = 0; x < sw; ++x)
-          run[(int64_t)j * sw + x] = j < S ? sl[((int64_t)j * sw + x) * ks] : tail[(int64_t)(j - S) * sw + x];
+    // reserve without pushing the cursor past pool_cap (a failed booking
+    // must not make every later booking of the launch fail too)
+    const unsigned long long o = pool_reserve(a.pool_cursor, need, a.pool_cap);
+    if (o == ~0ull) {
+      pool_failed = true;
+      if (ovf0) {          // the tail cannot be moved: the key keeps its state, the error is real
+        set_err(a.err, ERR_POOL);
+        return false;
+      }
+      return true;         // inline; ERR_POOL only if the list really outgrows S
     }
-  }
+    roff = o;
+    run = a.pool_wr + o * (uint64_t)sw;
+    const uint64_t* tail =
+        ovf0 ? (((ext0 >> 31) & 1ull) ? (const uint64_t*)a.pool_wr : a.pool_rd) + (ext0 >> 32) * (uint64_t)sw
+             : nullptr;
+    for (int j = 0; j < n; ++j)
+      for (int x = 0; x < sw; ++x)
+        run[(int64_t)j * sw + x] = j < S ? sl[((int64_t)j * sw + x) * st] : tail[(int64_t)(j - S) * sw + x];
+    st = 1;
+    CAP = (int)M;
+    return true;
+  };
+  auto list_full = [&]() { set_err(a.err, pool_failed ? ERR_POOL : ERR_PENDING); };
 #define NSLOT(j) (run ? run + (int64_t)(j) * sw : sl + (int64_t)(j) * sw * ks)
   auto copy_slot = [&](int dst, int src) {
     if (dst == src) return;
@@ -1458,6 +1484,7 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
     const uint32_t role = (uint32_t)(h >> 32) & 0xffu;
     const int stream = (int)((h >> 40) & 0xffu);
     const int64_t ts = rec_ts(rec, ts_base);
+    if (n >= CAP && !run && !grow(q)) return;
     int m = 0;
     if (!p.nfa_seq) {
       int nf = 0;   // advanced partials, staged in slots [CAP, 2 CAP)
@@ -1495,7 +1522,7 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
         }
       }
       if (m + nf > CAP) {
-        set_err(a.err, ERR_PENDING);
+        list_full();
         nf = CAP - m;
       }
       for (int f = 0; f < nf; ++f) copy_slot(m + f, CAP + f);
@@ -1530,7 +1557,7 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
           nfa_cond<kVm>(a, R, 0, role, nullptr, st, rec, ts_base)) {
         started = true;
         if (m >= CAP) {
-          set_err(a.err, ERR_PENDING);
+          list_full();
         } else {
           uint64_t* ns = NSLOT(m);
           ns[0] = (uint64_t)ts;
@@ -1551,7 +1578,7 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
       ovf = true;
       a.kext[idx] = (uint64_t)(uint32_t)n | (1ull << 31) | ((uint64_t)(roff + (unsigned long long)S) << 32);
     }
-  } else if (ovf0) {   // unreachable (an overflowed list always works in a run)
+  } else if (ovf0) {   // no record this window: the at-rest list (inline + tail run) stays as it is
     ovf = true;
   }
   const uint32_t nh = (uint32_t)(ovf ? S : n) | ((started ? 1u : 0u) << 8) | (ovf ? kHdrOvf : 0u);
@@ -1572,8 +1599,8 @@ __device__ void nfa_settle_runs(const WalkArgs& a, WalkLds& L, int bucket, int k
     uint64_t off = e >> 32;
     if (!((e >> 31) & 1ull)) {
       const unsigned long long cnt = n - (uint64_t)S;
-      const unsigned long long o = atomicAdd(a.pool_cursor, cnt);
-      if (o + cnt > a.pool_cap) {
+      const unsigned long long o = pool_reserve(a.pool_cursor, cnt, a.pool_cap);
+      if (o == ~0ull) {
         set_err(a.err, ERR_POOL);
         continue;
       }

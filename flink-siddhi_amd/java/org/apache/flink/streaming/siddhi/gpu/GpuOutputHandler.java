@@ -24,7 +24,9 @@ import org.apache.flink.types.Row;
  * sorted by attribute name (a TreeMap, :103-109), Row in definition order,
  * Tuple, POJO through Jackson, else IllegalArgumentException (:89).  Each
  * record is collected with the completing event's timestamp.  Rows arrive in
- * Siddhi's emission order (cep_options.ordered_output = 1).
+ * Siddhi's emission order (cep_options.ordered_output = 1).  STRING cells
+ * are dictionary ids resolved through the operator's cached {@link
+ * Dictionary}: a string seen before costs no JNI call and no new String.
  */
 final class GpuOutputHandler<R> implements CepNative.RowSink {
     private final String outputStreamId;
@@ -32,17 +34,17 @@ final class GpuOutputHandler<R> implements CepNative.RowSink {
     private final String[] names;
     private final int[] types;
     private final Output<StreamRecord<R>> output;
-    private final long op;   // string dictionary
+    private final Dictionary dict;   // the operator's string dictionary (cached: no JNI per cell)
     private final ObjectMapper objectMapper = new ObjectMapper();
 
     GpuOutputHandler(String outputStreamId, TypeInformation<R> typeInfo, String[] names, int[] types,
-                     Output<StreamRecord<R>> output, long op) {
+                     Output<StreamRecord<R>> output, Dictionary dict) {
         this.outputStreamId = outputStreamId;
         this.typeInfo = typeInfo;
         this.names = names;
         this.types = types;
         this.output = output;
-        this.op = op;
+        this.dict = dict;
         this.objectMapper.configure(DeserializationFeature.FAIL_ON_UNKNOWN_PROPERTIES, false);
     }
 
@@ -94,7 +96,7 @@ final class GpuOutputHandler<R> implements CepNative.RowSink {
             case ColumnBatch.BOOL:
                 return b.get(i) != 0;
             default:
-                return CepNative.operatorLookup(op, b.getInt(i * 4));
+                return dict.lookup(b.getInt(i * 4));
         }
     }
 }

@@ -43,8 +43,12 @@ import org.apache.flink.streaming.siddhi.schema.StreamSchema;
  * :301-313) and keeps its PriorityQueue private.
  *
  * Where the work goes:
- *   processEvent (SiddhiStreamOperator.java:52-54)  -> a row appended to the
- *       stream's columnar batch (ColumnBatch), no per-event send;
+ *   processEvent (SiddhiStreamOperator.java:52-54)  -> the record's fields
+ *       written straight into each reading plan's columnar batch (RowWriter
+ *       into ColumnBatch: no getRow boxing, no per-event send).  Everything
+ *       per (plan, stream) — the runtime, its input handle, the attribute
+ *       types, the batch — is resolved once when the plan starts, so an event
+ *       costs no JNI call and (for POJOs with primitive fields) no allocation;
  *   processElement, event time (:222-231)       -> full batches go to
  *       cep_buffer_batch: the device holds the out-of-order rows, not a
  *       PriorityQueue serialised on every event (:231);
@@ -81,9 +85,11 @@ public class GpuSiddhiStreamOperator<IN, OUT> extends AbstractStreamOperator<OUT
     private final long[] engineOptions;
 
     private transient long op;                                // cep_operator*
+    private transient Dictionary dict;                         // the operator's string dictionary
     private transient Map<String, ColumnBatch> batches;        // per (plan id, attribute layout)
-    private transient Map<String, Set<String>> plansOfStream;  // input stream -> plan ids reading it
-    private transient Map<String, Integer> inputs;             // (plan id, stream) -> cep_input handle
+    private transient Map<String, Map<String, Target>> planInputs;  // plan id -> stream -> target
+    private transient Map<String, Target[]> routes;            // input stream -> the plans reading it
+    private transient Map<String, RowWriter<IN>> writers;      // input stream -> field writer
     private transient List<CepNative.RowSink> sinks;           // kept reachable while native code holds them
     private transient ListState<byte[]> siddhiRuntimeState;
     private transient ListState<byte[]> queuedRecordsState;
@@ -111,9 +117,11 @@ public class GpuSiddhiStreamOperator<IN, OUT> extends AbstractStreamOperator<OUT
         final String[] err = new String[1];
         op = CepNative.operatorCreate(0, engineOptions, err);
         if (op == 0) throw new IllegalStateException("libcep: " + err[0]);
+        dict = new Dictionary(op);
         batches = new HashMap<>();
-        plansOfStream = new HashMap<>();
-        inputs = new HashMap<>();
+        planInputs = new HashMap<>();
+        routes = new HashMap<>();
+        writers = new HashMap<>();
         sinks = new ArrayList<>();
         for (String id : siddhiPlan.getExecutionPlanMap().keySet()) startPlan(id, false);
         if (restored != null) {
@@ -145,24 +153,35 @@ public class GpuSiddhiStreamOperator<IN, OUT> extends AbstractStreamOperator<OUT
             onEventReceived((ControlEvent) value.f1);
             return;
         }
-        // UndefinedStreamException for an unknown stream (SiddhiOperatorContext.java:151)
-        final StreamSchema<IN> schema = siddhiPlan.getInputStreamSchema(streamId);
+        final Target[] targets = routes.get(streamId);
+        if (targets == null) {
+            // UndefinedStreamException for an unknown stream (SiddhiOperatorContext.java:151);
+            // a known stream no plan reads is dropped
+            siddhiPlan.getInputStreamSchema(streamId);
+            return;
+        }
         final long ts = isProcessingTime ? System.currentTimeMillis() : element.getTimestamp();
-        final Set<String> plans = plansOfStream.get(streamId);
-        if (plans == null || plans.isEmpty()) return;   // no plan reads it
-        final Object[] row = schema.getStreamSerializer().getRow(value.f1);
+        final RowWriter<IN> w = writers.get(streamId);
         // every plan reading the stream gets the event (AbstractSiddhiOperator.java:283-287)
-        for (String id : plans) {
-            final long app = CepNative.operatorPlan(op, id);
-            final int[] types = inputTypes(app, streamId);
-            final String layout = layoutOf(types);
-            ColumnBatch b = batches.get(id + "|" + layout);
-            if (b == null) {
-                b = new ColumnBatch(app, layout, types, BATCH_ROWS, op);
-                batches.put(id + "|" + layout, b);
-            }
-            b.append(inputOf(id, app, streamId), row, ts);
-            if (b.full()) send(id, b);
+        for (int i = 0; i < targets.length; ++i) {
+            final Target t = targets[i];
+            final ColumnBatch b = t.batch;
+            w.write(value.f1, b, b.begin(t.input, ts));
+            b.commit();
+            if (b.full()) send(b);
+        }
+    }
+
+    /** One (plan, input stream) pair, resolved once in startPlan. */
+    private static final class Target {
+        final String planId;
+        final int input;          // cep_input handle
+        final ColumnBatch batch;  // the plan's batch for the stream's attribute layout
+
+        Target(String planId, int input, ColumnBatch batch) {
+            this.planId = planId;
+            this.input = input;
+            this.batch = batch;
         }
     }
 
@@ -181,28 +200,31 @@ public class GpuSiddhiStreamOperator<IN, OUT> extends AbstractStreamOperator<OUT
 
     /** A plan's batch to its runtime (disabled plans drop the rows at
      *  release time, as QueryRuntimeHandler.send does, :127-132). */
-    private void send(String id, ColumnBatch b) {
-        CepStatus.check(b.send(!isProcessingTime), CepNative.lastError(b.app));
+    private void send(ColumnBatch b) {
+        final int rc = b.send(!isProcessingTime);
+        if (rc != CepStatus.OK) CepStatus.check(rc, CepNative.lastError(b.app));
         b.clear();
-        if (isProcessingTime) flushOne(id);
+        if (isProcessingTime) {
+            final int f = CepNative.flush(b.app);
+            if (f != CepStatus.OK) CepStatus.check(f, CepNative.lastError(b.app));
+        }
     }
 
     private void sendAll() {
-        for (Map.Entry<String, ColumnBatch> e : batches.entrySet()) {
-            if (e.getValue().size() > 0) send(e.getKey().substring(0, e.getKey().lastIndexOf('|')), e.getValue());
+        for (ColumnBatch b : batches.values()) {
+            if (b.size() > 0) send(b);
         }
     }
 
-    private int inputOf(String id, long app, String streamId) {
-        final String k = id + "|" + streamId;
-        Integer h = inputs.get(k);
-        if (h == null) {
-            final int x = CepNative.input(app, streamId);
-            if (x < 0) CepStatus.check(-x, CepNative.lastError(app));
-            h = x;
-            inputs.put(k, h);
-        }
-        return h;
+    /** routes (stream -> targets) from planInputs, after a plan change. */
+    private void rebuildRoutes() {
+        final Map<String, List<Target>> m = new HashMap<>();
+        for (Map<String, Target> byStream : planInputs.values())
+            for (Map.Entry<String, Target> e : byStream.entrySet())
+                m.computeIfAbsent(e.getKey(), k -> new ArrayList<>()).add(e.getValue());
+        routes = new HashMap<>();
+        for (Map.Entry<String, List<Target>> e : m.entrySet())
+            routes.put(e.getKey(), e.getValue().toArray(new Target[0]));
     }
 
     private static String layoutOf(int[] types) {
@@ -247,29 +269,51 @@ public class GpuSiddhiStreamOperator<IN, OUT> extends AbstractStreamOperator<OUT
             System.arraycopy(names, 0, nm, 0, n[0]);
             System.arraycopy(types, 0, ty, 0, n[0]);
             final GpuOutputHandler<OUT> h = new GpuOutputHandler<>(e.getKey(), (TypeInformation<OUT>) e.getValue(), nm, ty,
-                                                                   (org.apache.flink.streaming.api.operators.Output) output, op);
+                                                                   (org.apache.flink.streaming.api.operators.Output) output, dict);
             sinks.add(h);
             CepStatus.check(CepNative.setCallback(app, e.getKey(), h), CepNative.lastError(app));
         }
         forget(id);
+        // resolve everything an event of each input stream needs, once
         final Set<String> layouts = new LinkedHashSet<>();
+        final Map<String, Target> byStream = new HashMap<>();
         for (String stream : CepNative.planInputStreams(plan).split("\n")) {
             if (stream.isEmpty()) continue;
-            plansOfStream.computeIfAbsent(stream, k -> new LinkedHashSet<>()).add(id);
-            layouts.add(layoutOf(inputTypes(app, stream)));
+            final int[] types = inputTypes(app, stream);
+            final String layout = layoutOf(types);
+            layouts.add(layout);
+            final int h = CepNative.input(app, stream);
+            if (h < 0) CepStatus.check(-h, CepNative.lastError(app));
+            ColumnBatch b = batches.get(id + "|" + layout);
+            if (b == null) {
+                b = new ColumnBatch(app, id, layout, types, BATCH_ROWS, dict);
+                batches.put(id + "|" + layout, b);
+            }
+            RowWriter<IN> w = writers.get(stream);
+            if (w == null) {
+                final StreamSchema<IN> schema = siddhiPlan.getInputStreamSchema(stream);
+                w = new RowWriter<>(schema);
+                writers.put(stream, w);
+            }
+            if (w.arity() != b.arity())
+                throw new IllegalArgumentException("stream " + stream + ": " + w.arity() + " fields, plan " + id
+                                                   + " defines " + b.arity() + " attributes");
+            byStream.put(stream, new Target(id, h, b));
         }
         // the device event-time buffer holds one attribute layout between two
         // watermarks (cep_buffer_batch): streams of one definition mix freely
         if (!isProcessingTime && layouts.size() > 1)
             throw new CepStatus.UnsupportedPlanException(
                 "plan " + id + " reads input streams of different definitions in event time");
+        planInputs.put(id, byStream);
+        rebuildRoutes();
     }
 
     /** A plan's routing entries, input handles and batches (removed / replaced). */
     private void forget(String id) {
-        for (Set<String> s : plansOfStream.values()) s.remove(id);
-        inputs.keySet().removeIf(k -> k.startsWith(id + "|"));
+        planInputs.remove(id);
         batches.keySet().removeIf(k -> k.startsWith(id + "|"));
+        rebuildRoutes();
     }
 
     @Override

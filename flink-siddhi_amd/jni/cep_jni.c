@@ -160,6 +160,7 @@ JNIEXPORT jint JNICALL FN(input)(JNIEnv* env, jclass cls, jlong app, jstring sid
 typedef struct {
   JavaVM* vm;
   jobject sink;
+  int failed;   /* receive threw: no more JNI work until the exception reaches Java */
   jmethodID receive;
   jclass bb;
   int ncols;
@@ -172,6 +173,13 @@ static void emit(void* user, const cep_rows* rows) {
   sink_ctx* c = (sink_ctx*)user;
   JNIEnv* env = NULL;
   if ((*c->vm)->GetEnv(c->vm, (void**)&env, JNI_VERSION_1_8) != JNI_OK || !env) return;
+  /* An exception thrown by an earlier receive is still pending: JNI calls
+   * other than the exception functions are undefined until it returns to Java
+   * (when cep_flush returns), so later callbacks of this flush do nothing. */
+  if (c->failed || (*env)->ExceptionCheck(env)) {
+    c->failed = 1;
+    return;
+  }
   const jlong n = rows->n;
   jobject ts = (*env)->NewDirectByteBuffer(env, (void*)rows->ts, n * 8);
   jobjectArray cols = (*env)->NewObjectArray(env, rows->ncols, c->bb, NULL);
@@ -181,6 +189,9 @@ static void emit(void* user, const cep_rows* rows) {
     (*env)->DeleteLocalRef(env, b);
   }
   (*env)->CallVoidMethod(env, c->sink, c->receive, n, ts, cols);
+  if ((*env)->ExceptionCheck(env)) {
+    c->failed = 1;   /* DeleteLocalRef is allowed with a pending exception */
+  }
   (*env)->DeleteLocalRef(env, cols);
   (*env)->DeleteLocalRef(env, ts);
 }
@@ -239,6 +250,9 @@ JNIEXPORT jint JNICALL FN(watermark)(JNIEnv* env, jclass cls, jlong app, jlong m
   return cep_watermark((cep_app*)(intptr_t)app, mark);
 }
 
+/* A RowSink exception propagates to Java when this returns; the sinks'
+ * failed flags are per sink, so a sink that threw stays silent for the rest of
+ * the operator's life (the Flink task fails on the exception anyway). */
 JNIEXPORT jint JNICALL FN(flush)(JNIEnv* env, jclass cls, jlong app) { return cep_flush((cep_app*)(intptr_t)app); }
 
 JNIEXPORT jbyteArray JNICALL FN(snapshot)(JNIEnv* env, jclass cls, jlong app) {

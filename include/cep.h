@@ -234,7 +234,12 @@ int cep_reset_output(cep_app* app);
 
 /* SiddhiAppRuntime.snapshot() — AbstractSiddhiOperator.java:374-380.
  * Restore is a TODO in the reference (AbstractSiddhiOperator.java:341);
- * cep_restore makes it real. */
+ * cep_restore makes it real.  A snapshot restores only into a runtime of the
+ * same compiled plan (plan hash and state geometry are checked; a mismatch is
+ * CEP_E_STATE naming the cause).  Compatibility note (round 4): two-state
+ * patterns whose s2 condition reads s1 compile to the N-state walk since
+ * round 4, so their snapshots from earlier builds are refused unless the
+ * restoring process sets CEP_PAIR_WALK=1 (the earlier two-state walk). */
 int cep_snapshot(cep_app* app, uint8_t** buf, size_t* len);
 int cep_restore(cep_app* app, const uint8_t* buf, size_t len);
 void cep_free(void* p);
@@ -307,7 +312,9 @@ int cep_route_batch_padded(cep_app* app, const cep_batch* batch, int world,
 int cep_send_records_padded(cep_app* app, const void* segs, int world,
                             int64_t seg_cap, int64_t events_represented);
 /* Make hip_stream wait for the routes queued so far (the route stream only:
- * the all-to-all of step s+1 need not wait for the walk of step s). */
+ * the all-to-all of step s+1 need not wait for the walk of step s).  A host
+ * batch's route runs on the engine stream and is joined into the route
+ * stream, so this also covers it. */
 int cep_route_signal(cep_app* app, void* hip_stream);
 /* Row shuffle for apps with several queries (sequences, aggregations, more
  * than one pattern; BASELINE config 5 across GPUs).  No predicate push-down:

@@ -150,3 +150,19 @@ def test_three_state_pool_lists_survive_snapshot():
     second = engine_rows(rt2.collect("O"))
     rt2.shutdown()
     assert_same_rows(first + second, want, "3-state snapshot with pool lists")
+
+
+def test_short_lists_in_large_chunks_book_no_pool():
+    # a key whose window holds more records than free
+    # slots used to book 2 x (n + records) pool slots up front, so a large
+    # chunk with few keys exhausted a small pool even though every list stays
+    # within its inline slots.  Lists here stay short (each C completes the
+    # advanced partials); 8 keys x ~37 k records per chunk would book ~600 k
+    # slots against a pool of 2^12: the flush must succeed, rows bit-exact.
+    plan = EV3 + (P3 + "from every s1=A[price > 0.5] -> s2=B -> s3=C within 1 sec "
+                  "select s1.k as k, s1.price as p1, s2.id as i2, s3.ts as t3 insert into O; end;")
+    w = three_streams(300000, 8)
+    want = oracle_run(plan, events(w)).get("O", [])
+    got = run(plan, w, pending_slots=16, chunk_events=1 << 22, pending_pool_log2=12)
+    assert len(want) > 10000
+    assert_same_rows(got, want, "short lists, large chunk, small pool")

@@ -50,3 +50,73 @@ def test_operator_shim_covers_the_reference_operator_hooks():
         assert re.search(r"public void %s\(" % hook, src), hook
     for state in ('"siddhiRuntimeState"', '"queuedRecordsState"'):
         assert state in src
+
+
+def _method_body(src, signature_re):
+    """Source of the method whose declaration matches signature_re (brace matched)."""
+    m = re.search(signature_re, src)
+    assert m, signature_re
+    i = src.index("{", m.end() - 1)
+    depth = 0
+    for j in range(i, len(src)):
+        depth += {"{": 1, "}": -1}.get(src[j], 0)
+        if depth == 0:
+            return src[i:j + 1]
+    raise AssertionError("unbalanced braces after " + signature_re)
+
+
+def _strip_throws(body):
+    # allocation on a failure path (building an exception) is not per-event work
+    return re.sub(r"throw new [^;]*;", "", body)
+
+
+def test_process_element_has_no_jni_and_no_allocation_per_event():
+    # VERDICT r04 item 7 (SURVEY §8 f1): the shim must replace getRow boxing
+    # (schema/StreamSerializer.java:38-82) and the per-event send
+    # (operator/SiddhiStreamOperator.java:52-54); everything per (plan,
+    # stream) is resolved once in startPlan
+    op = (JAVA / "GpuSiddhiStreamOperator.java").read_text()
+    body = _method_body(op, r"public void processElement\(")
+    assert "CepNative." not in body, "JNI call per event"
+    assert "getRow" not in body and "getStreamSerializer" not in body, "boxed Object[] row per event"
+    # the only calls outside the data path: the control-event branch and the
+    # unknown-stream check, both before the per-event loop
+    data = body[body.index("routes.get(streamId)"):]
+    data = data[data.index("return;", data.index("getInputStreamSchema")):]
+    assert "new " not in _strip_throws(data), "allocation per event"
+    assert "operatorPlan" not in body and "inputTypes" not in body and "streamSchema" not in body
+
+    w = (JAVA / "RowWriter.java").read_text()
+    write = _method_body(w, r"void write\(T input, ColumnBatch b, int r\)")
+    assert "new " not in _strip_throws(write).replace("new IllegalStateException(e.getMessage(), e)", "")
+    assert "CepNative." not in write
+    assert "getDeclaredField" not in write, "field accessors are resolved once, in the constructor"
+    for acc in ("getInt(", "getLong(", "getDouble(", "getFloat(", "getBoolean("):
+        assert acc in write, "primitive accessor %s (no boxing)" % acc
+
+    cb = (JAVA / "ColumnBatch.java").read_text()
+    for sig in (r"int begin\(int input, long timestamp\)", r"void commit\(\)", r"void putLong\(",
+                r"void putDouble\(", r"void putBool\(", r"void putObject\("):
+        b = _method_body(cb, sig)
+        assert "new " not in b and "CepNative." not in b, sig
+    d = (JAVA / "Dictionary.java").read_text()
+    intern = _method_body(d, r"int intern\(String s\)")
+    # JNI only after a cache miss
+    assert intern.index("ids.get(s)") < intern.index("CepNative.operatorIntern")
+
+
+def test_output_handler_resolves_strings_through_the_cached_dictionary():
+    h = (JAVA / "GpuOutputHandler.java").read_text()
+    assert "CepNative.operator" not in h, "per-cell JNI lookups on output"
+    assert "dict.lookup(" in h
+    d = (JAVA / "Dictionary.java").read_text()
+    look = _method_body(d, r"String lookup\(int id\)")
+    assert look.index("strings.get(id)") < look.index("CepNative.operatorLookup")
+
+
+def test_jni_emit_checks_for_a_pending_exception():
+    src = JNI.read_text()
+    emit = src[src.index("static void emit("):src.index("JNIEXPORT jint JNICALL FN(setCallback)")]
+    call = emit.index("CallVoidMethod")
+    assert "ExceptionCheck" in emit[:call], "no JNI work while an exception is pending"
+    assert "ExceptionCheck" in emit[call:], "receive's exception is noticed"
