@@ -87,6 +87,11 @@ def parse():
     ap.add_argument("--with-seq", action="store_true",
                     help="with --deliver: also deliver each row's arrival number (omitted by default, as the "
                          "reference's output handler does not read it)")
+    ap.add_argument("--ts-order", type=int, choices=[0, 1], default=1,
+                    help="cep_options.ts_order: 1 (default here) declares the input in event-time order -- the "
+                         "BASELINE generator's ts = T0 + i / R never decrease -- and runs the event-time fast "
+                         "paths; 0 runs the order-tolerant path (exact for timestamps in any order, the engine "
+                         "default)")
     ap.add_argument("--parity-steps", type=int, default=4,
                     help="config 5: steps of the stream the parity check covers (fresh state)")
     return ap.parse_args()
@@ -447,14 +452,14 @@ def main():
         plan = workload.PATTERN_PLAN
         opts = dict(device=local, key_capacity=(args.keys + world - 1) // world,
                     key_stride=world, key_offset=rank, chunk_events=args.chunk,
-                    profile=PROFILE_EVERY, ordered_output=0)
+                    profile=PROFILE_EVERY, ordered_output=0, ts_order=args.ts_order)
         if args.buckets_log2:
             opts["buckets_log2"] = args.buckets_log2
     elif config5:
         plan = workload.config5_plan()
         opts = dict(device=local, key_capacity=(args.keys + world - 1) // world, key_stride=world,
                     key_offset=rank, pending_slots=4, profile=PROFILE_EVERY, ordered_output=0,
-                    chunk_events=min(args.chunk, 1 << 24))
+                    chunk_events=min(args.chunk, 1 << 24), ts_order=args.ts_order)
     else:
         plan = workload.FILTER_PLAN
         opts = dict(device=local, profile=PROFILE_EVERY, ordered_output=0)
@@ -724,6 +729,8 @@ def main():
                         "keys": args.keys, "keys_dist": args.keys_dist if args.keys_dist == "uniform" else "zipf(s=1.1)",
                         "events_per_step_per_gpu": n, "rate_per_ms": args.rate,
                         "chunk_events": args.chunk, "parallelism": "key-sharded x%d" % world,
+                        "ts_order": ("event-time order (ts_order=1: event-time fast paths)" if args.ts_order
+                                     else "any order (ts_order=0: order-tolerant path)"),
                         "ingest": (("%s all-to-all key shuffle (%s)" % ("rccl" if _coll_device() == "cuda"
                                                                          else "gloo host-staged",
                                                                          "padded segments, in-band counts"

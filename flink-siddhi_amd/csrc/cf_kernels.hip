@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
       fkey[e] = (uint64_t)(uint32_t)hv[e];
     }
     if (p.within >= 0) {
-      const int64_t before = row0 > 0 ? (int64_t)a.in_recs[(row0 - 1) * rw + 2] : a.rows.prev_ts;
+      const int64_t before = row0 > 0 ? (int64_t)a.in_recs[(row0 - 1) * rw + 2] : batch_prev_ts(a.rows);
       bool bad = false;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
         const int64_t prev = lane > 0 ? (int64_t)up : (e > 0 ? (int64_t)last : before);
         if ((valid >> e) & 1u) bad |= (int64_t)tsv[e] < prev;
       }
-      if (bad) set_err(a.err, ERR_ORDER);
+      if (bad) report_descent(a.rows, a.err);
     }
   }
   if (!FR && valid) {
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
     if (p.within >= 0) {
       // event-time order check (`within` pruning relies on it): row r - 1 is
       // held by the previous lane (same e), lane 63 (e - 1), or loaded
-      const int64_t before = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
+      const int64_t before = row0 > 0 ? a.rows.ts[row0 - 1] : batch_prev_ts(a.rows);
       bool bad = false;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
         const int64_t prev = lane > 0 ? (int64_t)up : (e > 0 ? (int64_t)last : before);
         if ((valid >> e) & 1u) bad |= (int64_t)tsv[e] < prev;
       }
-      if (bad) set_err(a.err, ERR_ORDER);
+      if (bad) report_descent(a.rows, a.err);
     }
     const uint32_t all = (1u << E) - 1u;
     if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E, NP>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
@@ -279,7 +279,8 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
     const uint32_t role = packed[e] >> 25;
     const uint32_t slot = hist[b] + (packed[e] & 0x1fffu);
     const int64_t dts = (int64_t)tsv[e] - ts_base;
-    if (dts < 0 || dts > 0xffffffffll) set_err(a.err, ERR_ORDER);
+    if (dts < 0) report_descent(a.rows, a.err);
+    else if (dts > 0xffffffffll) set_err(a.err, ERR_TS_SPAN);
     const uint64_t w0 = (uint64_t)(uint32_t)dts | ((uint64_t)(wave * 64 * E + 64 * e + lane) << 32) |
                         ((uint64_t)role << 45) | ((uint64_t)lkey[e] << 48);
     const uint64_t c0 = fc0[e], c1 = fc1[e];

@@ -12,6 +12,22 @@ __device__ __forceinline__ void set_err(unsigned int* err, unsigned int bit) {
   if (err) atomicOr(err, bit);
 }
 
+// ts of the row before a batch's first row (host-known, or the device word
+// the previous batch left: RowsArgs::prev_ts_dev).
+__device__ __forceinline__ int64_t batch_prev_ts(const RowsArgs& r) {
+  int64_t p = r.prev_ts;
+  if (r.prev_ts_dev) {
+    const int64_t d = *r.prev_ts_dev;
+    p = d > p ? d : p;
+  }
+  return p;
+}
+
+// A ts descent in a slice that promised event-time order (ts_order = 1).
+__device__ __forceinline__ void report_descent(const RowsArgs&, unsigned int* err) {
+  set_err(err, ERR_ORDER);
+}
+
 // Workgroup barrier that orders LDS only.  __syncthreads() also releases
 // global memory, which makes every wave drain its outstanding global loads
 // and stores (s_waitcnt vmcnt(0)) before the barrier; phases that only hand

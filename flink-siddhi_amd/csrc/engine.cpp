@@ -152,6 +152,9 @@ struct PatternRT {
       hot_active;
   HostBuf hot_active_host;     // pinned: slots in use (read without a sync)
   hipEvent_t hot_fork = nullptr, hot_join = nullptr;   // hot kernels on the side stream, beside the walk
+  // a pattern whose result depends on event-time order (`within`, not a
+  // sequence): with cep_options.ts_order = 0 it runs the order-tolerant path
+  bool order_sensitive = false;
 };
 
 // Multi-query group (mq_kernels.hip): keyed queries of one app sharing a
@@ -246,6 +249,8 @@ struct cep_app {
   } ro;
   int64_t events_in = 0, matches_out = 0, batches = 0, late_events = 0;
   int64_t last_ts = INT64_MIN;
+  DevBuf last_ts_dev;          // last ts of the previous batch (RowsArgs::prev_ts_dev)
+  bool force_tolerant = false; // this batch holds late rows (cep_watermark, late_policy 2)
   int64_t launches[16] = {0};
   double kernel_ms[16] = {0};
   int64_t kernel_timed[16] = {0};
@@ -1025,8 +1030,9 @@ int create_runtime(cep_app* a) {
         p.cap_null[i] = str ? ~0ull : 0ull;
       }
     }
-    // NFA patterns stage advanced partials in a second bank of S slots
-    const int bank = q.nfa ? 2 : 1;
+    // NFA patterns stage advanced partials in a second bank of S slots (so do
+    // the order-tolerant runs of a 2-state pattern with `within`: nfa_pair)
+    const int bank = (q.nfa || (q.within >= 0 && !agg)) ? 2 : 1;
     const bool keyed = q.key_col_a >= 0;
     int64_t kcap = keyed ? a->opt.key_capacity : 1;
     p.key_capacity = kcap;
@@ -1190,7 +1196,18 @@ int create_runtime(cep_app* a) {
       hipMemset(rt.kcount.p, 0, 4);
       hipMemset((char*)rt.kcount.p + 4, 0xff, 4);
     }
+    // `within` makes a pattern's result depend on event-time order (App. A.3
+    // prunes on every event of the waiting state's stream); a sequence keeps
+    // every row of its streams and prunes by |ts - ts(s1)| in any order, an
+    // aggregation has no window: neither needs the re-run
+    rt.order_sensitive = p.within >= 0 && !agg && !(q.nfa && q.sequence);
     a->pats.push_back(rt);
+  }
+  {
+    const int64_t none = INT64_MIN;
+    if (!dev_ensure(&a->last_ts_dev, 64, a->stream, false) ||
+        hipMemcpy(a->last_ts_dev.p, &none, 8, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(a, CEP_E_DEVICE, "out of device memory");
   }
   if (std::getenv("CEP_STAMPS") && !dev_ensure(&a->stamps, (size_t)2 * 4096 * 16 * 8, a->stream, false))
     return fail(a, CEP_E_DEVICE, "out of device memory (stamps)");
@@ -1226,7 +1243,8 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
   const int64_t ntiles = (rows.n + kTile - 1) / kTile;
   if (ntiles == 0) return CEP_OK;
   // look-back words for k_filter's or k_filterc's (smaller) tiles
-  const int64_t nflags = std::max<int64_t>(ntiles, (rows.n + filterc_rows_per_tile() - 1) / filterc_rows_per_tile());
+  const int64_t fcr = filterc_rows_per_tile();
+  const int64_t nflags = std::max<int64_t>(ntiles, (rows.n + fcr - 1) / fcr);
   if (!dev_ensure(&a->tile_state, (size_t)nflags * 8, a->stream, false))
     return fail(a, CEP_E_DEVICE, "out of device memory (tile state)");
   hipMemsetAsync(a->tile_state.p, 0, (size_t)nflags * 8, a->stream);
@@ -1274,6 +1292,8 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
       fc = al(rows.cols.p[fa.pcol[k]], type_width(rows.cols.t[fa.pcol[k]]));
     if (fc && rows.stream) fc = al(rows.stream, 1);
   }
+  // arrival numbers are written only when someone reads them
+  fa.write_seq = (a->opt.omit_seq && !a->opt.ordered_output) ? 0 : 1;
   LaunchTimer t(a, CEP_K_FILTER);
   if (fc) {
     const int64_t tr = filterc_rows_per_tile();
@@ -1531,14 +1551,68 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
   return CEP_OK;
 }
 
-int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
-                const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
+// The order-tolerant form of a pattern (rows whose ts may go backwards).
+// Every row of the waiting state's stream may expire partials, so the
+// partition keeps them all; the walk's closed form (event-time order, only
+// g-passing B's) is off.  A 2-state pattern is walked by the N-state walk on
+// its own record roles and state layout (nfa_pair): that walk keeps lists
+// longer than pending_slots in the pending pool, as the closed-form path does.
+PatternArgs tolerant_args(const PatternRT& rt, const Query& q) {
+  PatternArgs p = rt.pa;
+  p.tolerant = 1;
+  p.closed_form = 0;
+  if (!p.nfa_mode && !p.agg_mode) {
+    p.nfa_mode = 1;
+    p.nfa_pair = 1;
+    p.nfa_seq = 0;
+    p.nstates = 2;
+    p.st_stream[0] = q.a_stream;
+    p.st_stream[1] = q.b_stream;
+    for (int j = 0; j < 2; ++j) {
+      p.st_min[j] = p.st_max[j] = 1;
+      p.st_raw[j] = -1;
+      p.st_walk[j] = -1;
+    }
+    p.st_tail_opt[0] = 0;
+    p.st_tail_opt[1] = 1;
+    p.stream_mask = (1 << q.a_stream) | (1 << q.b_stream);
+    for (int i = 0; i < 8; ++i) p.key_col_s[i] = -1;
+    p.key_col_s[q.a_stream] = q.key_col_a;
+    p.key_col_s[q.b_stream] = q.key_col_b;
+    for (int i = 0; i < p.ncap; ++i) {   // s1's captures, from the A record
+      p.cap_state[i] = 0;
+      p.cap_index[i] = -1;
+      p.cap_word[i] = p.cap_from_rec[i];
+      p.cap_null[i] = 0;
+    }
+  }
+  return p;
+}
+
+// tolerant: run on the order-tolerant path (rows whose ts may go backwards:
+// a watermark release holding late rows, or the re-run after a descent).
+int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_in,
+                const uint64_t* in_recs = nullptr, int in_rec_words = 0, bool tolerant = false) {
   const Query& q = a->app.queries[rt.q];
   OutStream& o = a->outs[a->app.output_index(q.out_stream)];
   if (o.bound == 0) o.bound = rt.extra_bound;
-  o.bound += rows_all.n;
+  o.bound += rows_in.n;
   int rc = ensure_out_cap(a, o, o.bound);
   if (rc) return rc;
+  // Timestamps in any order (cep_options.ts_order = 0): a pattern with
+  // `within` runs the order-tolerant path, whose state is exactly the
+  // oracle's (App. A.3: partials pruned only by |ts - ts(s1)| > W on events
+  // of the stream they wait on); the event-time fast paths (closed form,
+  // push-down of g-failing B's, pruning at A arrivals) need ts_order = 1.
+  // A sequence prunes by |ts - ts(s1)| on every row of its streams in any
+  // order: tolerant only drops its order check.  The multi-GPU record / row
+  // shuffles always take the event-time paths.
+  if (!tolerant && a->opt.ts_order == 0 && rt.pa.within >= 0 && (rt.order_sensitive || rt.pa.nfa_seq) &&
+      !in_recs && !rows_in.seq)
+    tolerant = true;
+  const RowsArgs& rows_all = rows_in;
+  if (rt.sparse && tolerant)
+    return fail(a, CEP_E_UNSUPPORTED, "sparse_keys with out-of-order timestamps under `within`");
   if (rt.sparse) {
     // partition values -> dense slots (keymap.hip); the pattern then reads
     // the dense column in place of the key column
@@ -1577,7 +1651,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
       return fail(a, CEP_E_ARG, "sparse_keys needs 16-byte aligned columns");
     return run_pattern_cf(a, rt, q, o, rows, cf);
   }
-  if (rt.cf && !rows_all.seq && (in_recs || pref_aligned(rt.pref, rows_all))) {
+  if (rt.cf && !tolerant && !rows_all.seq && (in_recs || pref_aligned(rt.pref, rows_all))) {
     CfPlan cf;
     if (cf_plan(rt, rows_all, &cf, in_recs != nullptr))
       return run_pattern_cf(a, rt, q, o, rows_all, cf, in_recs, in_rec_words);
@@ -1610,7 +1684,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
     if (pa.pref.n >= 0 && !pref_aligned(pa.pref, rows)) pa.pref.n = -1;
     if (r0 > 0) pa.rows.prev_ts = INT64_MIN;
     pa.vm = {(const Ins*)a->code.p, (const uint64_t*)a->konst.p};
-    pa.pat = rt.pa;
+    pa.pat = tolerant ? tolerant_args(rt, q) : rt.pa;
     pa.tile_rows = kPartThreads * kPartItems;
     pa.recs = (uint64_t*)rt.recs[b].p;
     pa.tile_off = (uint16_t*)rt.tile_off[b].p;
@@ -1626,7 +1700,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
     hipStreamWaitEvent(a->stream, rt.part_done[b], 0);
     WalkArgs wa{};
     wa.vm = pa.vm;
-    wa.pat = rt.pa;
+    wa.pat = pa.pat;
     wa.recs = pa.recs;
     wa.tile_off = pa.tile_off;
     wa.ntiles = (int)ntiles;
@@ -1641,7 +1715,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
     wa.kstride = rt.kstride;
     wa.out = out_args(o, q);
     wa.err = pa.err;
-    const bool pool = q.nfa && rt.kext.p;
+    const bool pool = (q.nfa || pa.pat.nfa_pair) && rt.kext.p;
     if (pool) {
       wa.kext = (uint64_t*)rt.kext.p;
       wa.pool_rd = (const uint64_t*)rt.pool[rt.pool_side].p;
@@ -1652,7 +1726,7 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_all,
     }
     {
       LaunchTimer t(a, CEP_K_WALK);
-      launch_walk(wa, P, rt.walk_vm, a->stream);
+      launch_walk(wa, P, rt.walk_vm || pa.pat.nfa_pair, a->stream);
     }
     if (pool) rt.pool_side ^= 1;   // this launch's write pool holds every run now
     hipEventRecord(rt.walk_done[b], a->stream);
@@ -1721,7 +1795,9 @@ int run_mq(cep_app* a, MqRT& g, const RowsArgs& rows_all) {
   for (int s = 0; s < 8; ++s) pa.ncond[s] = g.ncond[s];
   pa.conds = (const MqCond*)g.dconds.p;
   pa.nphys = nphys;
-  pa.check_order = g.check_order ? 1 : 0;
+  // the group's sequences prune by |ts - ts(s1)| on every row of their
+  // streams (any order); the check stays for callers that asked for it
+  pa.check_order = (g.check_order && a->opt.ts_order == 1 && !a->force_tolerant) ? 1 : 0;
   pa.key_capacity = g.key_capacity;
   pa.key_stride = g.key_stride;
   pa.key_offset = g.key_offset;
@@ -1798,12 +1874,17 @@ int send_device_rows(cep_app* a, const RowsArgs& rows) {
       rc = run_filter(a, q, rows);
     } else if (q.kind == Q_PATTERN || q.kind == Q_AGG) {
       for (auto& rt : a->pats)
-        if (rt.q == (int)qi) rc = run_pattern(a, rt, rows);
+        if (rt.q == (int)qi) rc = run_pattern(a, rt, rows, nullptr, 0, a->force_tolerant);
     }
     if (rc) return rc;
   }
+  // the batch's last ts: the next batch's first-row order check (device
+  // batches; the host does not see their ts)
+  if (rows.n > 0 && rows.prev_ts_dev)
+    hipMemcpyAsync(a->last_ts_dev.p, rows.ts + rows.row0 + rows.n - 1, 8, hipMemcpyDeviceToDevice, a->stream);
   return CEP_OK;
 }
+
 
 int device_error(cep_app* a, unsigned int e);
 
@@ -1862,6 +1943,8 @@ void cep_default_options(cep_options* o) {
   o->key_stride = 1;
   o->key_offset = 0;
   o->pending_pool_log2 = 20;
+  o->late_policy = 2;
+  o->ts_order = 0;
 }
 
 int cep_validate(const char* plan, char* err, size_t errlen) {
@@ -2131,6 +2214,7 @@ void cep_destroy(cep_app* a) {
     dev_free(b);
   dev_free(&a->code);
   dev_free(&a->konst);
+  dev_free(&a->last_ts_dev);
   dev_free(&a->tile_state);
   dev_free(&a->route_arena);
   dev_free(&a->route_tcount);
@@ -2222,6 +2306,7 @@ int batch_rows(cep_app* a, const cep_batch* b, RowsArgs* out, int* slot, bool* d
   rows.n = b->n;
   rows.seq0 = a->events_in;
   rows.prev_ts = a->last_ts;
+  rows.prev_ts_dev = (const int64_t*)a->last_ts_dev.p;
   if (b->on_device) {
     for (int c = 0; c < b->ncols; ++c) rows.cols.p[c] = b->cols[c];
     rows.ts = b->ts;
@@ -2379,12 +2464,16 @@ int cep_watermark(cep_app* a, int64_t mark) {
   const int64_t rel = hb[0];
   if (rel == 0) return CEP_OK;
   // A row older than an earlier watermark's release arrived late.  The
-  // reference hands it to Siddhi out of order (AbstractSiddhiOperator.java:
-  // 238-245); `within` needs event-time order, so late rows are dropped (as
-  // Flink drops late elements) and counted in cep_stats.late_events; the
-  // on-time rows are released and the buffer stays consistent.
-  const int64_t late = any_released ? std::min(hb[3], rel) : 0;
-  a->late_events += late;
+  // reference offers it to its PriorityQueue like any row, and this
+  // watermark's drain hands it to Siddhi first (smallest ts), behind rows it
+  // has already processed (AbstractSiddhiOperator.java:222-231, 238-245).
+  // late_policy 2 (default) does the same: the released prefix, late rows
+  // included, in (ts, arrival) order, on the order-tolerant path.  Policies
+  // 0 / 1 drop them (counted in cep_stats.late_events).
+  const int64_t late_n = any_released ? std::min(hb[3], rel) : 0;
+  a->late_events += late_n;
+  const bool deliver_late = a->opt.late_policy == 2;
+  const int64_t late = deliver_late ? 0 : late_n;   // rows dropped from the release
   const int32_t* perm = (const int32_t*)r.idx_out.p;
   bool ok = true;
   for (int c = 0; c < nc && ok; ++c) {
@@ -2424,7 +2513,9 @@ int cep_watermark(cep_app* a, int64_t mark) {
   bb.on_device = 1;
   a->last_ts = r.released_max;   // the kernel's order check spans the watermark
   const int64_t rmax = hb[2];
+  a->force_tolerant = deliver_late && late_n > 0;
   int rc = cep_send_batch(a, &bb);
+  a->force_tolerant = false;
   if (rc == CEP_OK) r.released_max = std::max(r.released_max, rmax);
   // the sorted batch buffers are reused by the next watermark: finish first
   hipStreamSynchronize(a->stream);
@@ -2566,7 +2657,8 @@ int cep_output_device(cep_app* a, const char* out_id, cep_rows* rows) {
   rows->n = (int64_t)cnt;
   rows->ncols = (int32_t)o.cols.size();
   rows->ts = (const int64_t*)o.ts.p;
-  rows->seq = (const int64_t*)o.seq.p;
+  // omit_seq with unordered output: the kernels need not write them
+  rows->seq = (a->opt.omit_seq && !a->opt.ordered_output) ? nullptr : (const int64_t*)o.seq.p;
   rows->cols = ptrs.data();
   return CEP_OK;
 }

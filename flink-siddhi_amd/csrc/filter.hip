@@ -1,20 +1,23 @@
-// k_filterc — `from S[expr] select attrs insert into O` as one coalesced
-// stream-compaction pass (the per-event filter branch of
+// k_filterc — `from S[expr] select attrs insert into O` as one
+// coalesced stream-compaction pass (the per-event filter branch of
 // operator/AbstractSiddhiOperator.java:130 -> Siddhi's FilterProcessor, for
 // term-list predicates and plain attribute projections; k_filter keeps the
 // rest).
 //
-// Layout of a 2048-row tile: wave w owns rows [512 w, 512 w + 512); lane l
-// holds row pairs 128 i + 2 l + {0, 1}, i < 4, so every load instruction of a
-// predicate column reads one contiguous 512 B (4-byte column) or 1 KiB
-// (8-byte column) span: a wave's loads are fully coalesced, and all of a
-// lane's predicate loads are issued before the first is used.  Selected rows
-// are compacted per wave (DPP scans of per-pair counts, four pairs packed per
-// word), then the projection runs lane per selected row, so each output
-// column is written as consecutive rows by consecutive lanes.  The global
-// output position comes from a decoupled look-back over tile tickets; the
+// Layout of a tile: 1024 lanes, wave w owns rows [2 P 64 w, 2 P 64 (w + 1));
+// lane l holds row pairs 128 i + 2 l + {0, 1}, i < P (P = 4: 8192-row
+// tiles), so every load instruction of a column reads one contiguous 512 B
+// (4-byte column) or 1 KiB (8-byte column) span: a wave's loads are fully
+// coalesced, and all of a lane's loads are issued before the first is used.
+// Selected rows are ranked per wave (DPP scans of per-pair counts, four pairs
+// packed per word); the global output position comes from a decoupled
+// look-back over tile tickets.
+//
+// Selected rows are compacted
+// per wave in LDS, then the projection runs lane per selected row, so each
+// output column is written as consecutive rows by consecutive lanes; the
 // projection's loads for the first 64 selected rows of every wave are in
-// flight while it runs.
+// flight while the look-back runs.
 #include <hip/hip_runtime.h>
 
 #include "dev_common.h"
@@ -40,8 +43,8 @@ constexpr int kFcWaves = kFcThreads / 64;
 #define FC_MINW 4
 #endif
 constexpr int kFcPairs = FC_PAIRS;               // row pairs per lane
-constexpr int kFcWaveRows = 64 * 2 * kFcPairs;   // 512
-constexpr int kFcTile = kFcWaves * kFcWaveRows;  // 2048
+constexpr int kFcWaveRows = 64 * 2 * kFcPairs;   // 512 rows per wave
+constexpr int kFcTile = kFcWaves * kFcWaveRows;  // 8192
 constexpr int kFcRegCols = FC_REGCOLS;                    // projected columns loaded ahead of the look-back
 constexpr uint64_t kFcStatusShift = 62;
 constexpr uint64_t kFcValueMask = (1ull << 62) - 1;
@@ -70,6 +73,55 @@ __device__ __forceinline__ void fc_load_pair(const void* p, int type, int64_t r,
   }
 }
 
+// Decoupled look-back (one wave): lane l reads the flag of tile base - l;
+// publishes this tile's aggregate, then its inclusive prefix; *s_prefix gets
+// the rows of every earlier tile.
+__device__ __forceinline__ void fc_lookback(const FilterArgs& a, int64_t tile, uint32_t total, int lane,
+                                            unsigned long long* s_prefix) {
+  unsigned long long* flags = a.tile_state;
+  unsigned long long prefix = 0;
+  if (tile == 0) {
+    prefix = __hip_atomic_load(a.out.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (lane == 0)
+      __hip_atomic_store(&flags[tile], (1ull << kFcStatusShift) | total, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    int64_t b = tile - 1;
+    unsigned spins = 0;
+    while (true) {
+      const int64_t j = b - lane;
+      const unsigned long long v =
+          j >= 0 ? __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      const uint32_t st = (uint32_t)(v >> kFcStatusShift);
+      const uint64_t ready = __ballot(st != 0);
+      const uint64_t incl = __ballot(st == 2);
+      const int f = incl ? __ffsll((long long)incl) - 1 : 63;
+      const uint64_t need = f == 63 ? ~0ull : ((2ull << f) - 1ull);   // lanes 0..f
+      if ((ready & need) != need) {
+        if (++spins > (1u << 22)) {   // a predecessor never published: fail loudly
+          if (lane == 0) set_err(a.err, ERR_WINDOW);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      unsigned long long x = ((need >> lane) & 1ull) ? (v & kFcValueMask) : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+      prefix += x;
+      if (incl) break;
+      b -= 64;
+    }
+  }
+  if (lane == 0) {
+    __hip_atomic_store(&flags[tile], (2ull << kFcStatusShift) | (prefix + total), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    *s_prefix = prefix;
+    if (tile == (int64_t)gridDim.x - 1)
+      __hip_atomic_store(a.out.count, prefix + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 }  // namespace
 
 template <int Q>   // distinct predicate columns (1..3)
@@ -79,13 +131,9 @@ __global__ __launch_bounds__(kFcThreads, FC_MINW) void k_filterc(FilterArgs a) {
   __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_prefix;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef FC_NOTICKET   // experiment: tiles in dispatch order (the look-back's spin limit bounds a stall)
-  const int64_t tile = blockIdx.x;
-#else
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
   __syncthreads();
   const int64_t tile = s_tile;
-#endif
   const int64_t n = a.rows.n;
   const int64_t wrow0 = tile * kFcTile + (int64_t)wave * kFcWaveRows;   // slice-relative
   const int64_t brow0 = a.rows.row0 + wrow0;                            // batch row
@@ -187,51 +235,8 @@ __global__ __launch_bounds__(kFcThreads, FC_MINW) void k_filterc(FilterArgs a) {
   };
   if ((uint32_t)lane < wt) load_row((uint32_t)lane);
 
-  // ---- decoupled look-back (wave 0): lane l reads the flag of tile base - l
-  if (wave == 0) {
-    unsigned long long* flags = a.tile_state;
-    unsigned long long prefix = 0;
-    if (tile == 0) {
-      prefix = __hip_atomic_load(a.out.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0)
-        __hip_atomic_store(&flags[tile], (1ull << kFcStatusShift) | total, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      int64_t b = tile - 1;
-      unsigned spins = 0;
-      while (true) {
-        const int64_t j = b - lane;
-        const unsigned long long v =
-            j >= 0 ? __hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        const uint32_t st = (uint32_t)(v >> kFcStatusShift);
-        const uint64_t ready = __ballot(st != 0);
-        const uint64_t incl = __ballot(st == 2);
-        const int f = incl ? __ffsll((long long)incl) - 1 : 63;
-        const uint64_t need = f == 63 ? ~0ull : ((2ull << f) - 1ull);   // lanes 0..f
-        if ((ready & need) != need) {
-          if (++spins > (1u << 22)) {   // a predecessor never published: fail loudly
-            if (lane == 0) set_err(a.err, ERR_WINDOW);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        unsigned long long x = ((need >> lane) & 1ull) ? (v & kFcValueMask) : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        prefix += x;
-        if (incl) break;
-        b -= 64;
-      }
-    }
-    if (lane == 0) {
-      __hip_atomic_store(&flags[tile], (2ull << kFcStatusShift) | (prefix + total), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      s_prefix = prefix;
-      if (tile == (int64_t)gridDim.x - 1)
-        __hip_atomic_store(a.out.count, prefix + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  // ---- decoupled look-back (wave 0)
+  if (wave == 0) fc_lookback(a, tile, total, lane, &s_prefix);
   __syncthreads();
   const int64_t obase = (int64_t)s_prefix + woff;
   // ---- stores: consecutive lanes -> consecutive output rows
@@ -250,13 +255,15 @@ __global__ __launch_bounds__(kFcThreads, FC_MINW) void k_filterc(FilterArgs a) {
           store_col(a.out.col[c], a.out.type[c], pos, load_col(a.rows.cols.p[col], a.rows.cols.t[col], row));
         }
         a.out.ts[pos] = vts;
-        a.out.seq[pos] = vseq;
+        if (a.write_seq) a.out.seq[pos] = vseq;
       }
     }
   }
 }
 
 int filterc_rows_per_tile() { return kFcTile; }
+
+
 
 void launch_filterc(const FilterArgs& a, int64_t ntiles, hipStream_t s) {
   switch (a.npref) {

@@ -29,6 +29,10 @@ struct RowsArgs {
   int64_t prev_ts;         // ts of the row before the slice (monotonicity check)
   const int64_t* seq;      // per-row arrival numbers (rows received through the row
                            // shuffle, cep_send_rows), or nullptr: seq0 + row
+  // Event-time order check (patterns with `within`, cep_options.ts_order =
+  // 1): device word with the last ts of the previous batch (device batches:
+  // the host does not see their ts), nullptr: none.
+  const int64_t* prev_ts_dev;
 };
 
 __device__ __forceinline__ int64_t row_seq(const RowsArgs& r, int64_t row) {
@@ -88,6 +92,7 @@ struct FilterArgs {
   int32_t npref;
   int32_t pcol[kPref];
   int32_t fslot[kMaxTerms];
+  int32_t write_seq;       // 0: the output's arrival numbers are not needed (omit_seq, unordered)
 };
 
 // ------------------------------------------------------- keyed pattern --
@@ -113,6 +118,9 @@ struct PatternArgs {
   int32_t key_stride, key_offset;   // shard ownership (key % stride == offset)
   int32_t buckets_log2;
   int32_t closed_form;     // 1: every && g independent of s1 -> data-parallel walk
+  int32_t tolerant;        // 1: ts in any order (App. A.3 |ts(B) - ts(s1)| > W on every
+                           // event of the waiting state's stream): keep every row of those
+                           // streams, no pruning at A arrivals, no order check
   // group-by / having (agg_mode = 1): per-key running aggregates; state slot 0
   // holds (accumulator, count) word pairs per aggregate
   int32_t agg_mode;
@@ -125,6 +133,9 @@ struct PatternArgs {
   // N-state pattern / sequence (nfa_mode = 1): one NFA lane per key; a
   // partial is a state slot {start ts, state | count << 8, captures...}
   int32_t nfa_mode;
+  int32_t nfa_pair;                // 1: a 2-state pattern's records and state layout (roles
+                                   // A / B / G, slots {ts, -, s1 captures}) walked by the
+                                   // N-state walk (order-tolerant runs: pool-backed lists)
   int32_t nfa_seq;                 // 1: sequence (strict contiguity, count states)
   int32_t nstates;
   int32_t stream_mask;             // input handles the query reads

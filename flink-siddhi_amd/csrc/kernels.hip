@@ -428,7 +428,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
                            : 0;
         }
       }
-      int64_t prev = row0 > 0 ? prev_ld : a.rows.prev_ts;
+      int64_t prev = row0 > 0 ? prev_ld : batch_prev_ts(a.rows);
       uint32_t is_a = 0, is_b = 0;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
           is_b |= (sid[e] == p.b_stream ? 1u : 0u) << e;
         }
       }
-      if (p.within >= 0) {   // event-time order check (`within` pruning relies on it)
+      if (p.within >= 0 && !p.tolerant) {   // event-time order check (`within` pruning relies on it)
         bool bad = false;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
             prev = (int64_t)tsv[e];
           }
         }
-        if (bad) set_err(a.err, ERR_ORDER);
+        if (bad) report_descent(a.rows, a.err);
       }
       const uint32_t all = (1u << E) - 1u;
       if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
@@ -455,8 +455,9 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
         if (p.g_walk_prog >= 0) {
           role_b = is_b;
         } else {
-          role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
-          role_g = role_b;
+          role_g = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
+          // tolerant: a g-failing B still prunes (|ts(B) - ts(s1)| > W)
+          role_b = p.tolerant ? is_b : role_g;
         }
       }
 #pragma unroll
@@ -473,10 +474,10 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
           is_b |= (sid[e] == p.b_stream ? 1u : 0u) << e;
         }
       }
-      if (p.within >= 0) {   // event-time order check (`within` pruning relies on it)
+      if (p.within >= 0 && !p.tolerant) {   // event-time order check (`within` pruning relies on it)
         uint64_t t[E];
         load_run<E>(a.rows.ts, T_LONG, row0, nvalid, t);
-        int64_t prev = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
+        int64_t prev = row0 > 0 ? a.rows.ts[row0 - 1] : batch_prev_ts(a.rows);
         bool bad = false;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -485,10 +486,10 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
             prev = (int64_t)t[e];
           }
         }
-        if (bad) set_err(a.err, ERR_ORDER);
+        if (bad) report_descent(a.rows, a.err);
       }
       bool nfa = false;
-      if constexpr (kVm) nfa = p.nfa_mode != 0;
+      if constexpr (kVm) nfa = p.nfa_mode != 0 && !p.nfa_pair;
       if (nfa) {
         // N-state pattern / sequence: role bit j = state j's own condition
         // accepts the row (or it is checked in the walk); bit 7 = row kept.
@@ -505,7 +506,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
               if (p.st_raw[j] < 0 || eval_pred(a.vm, p.st_raw[j], R, RowEnv{&a.rows, row0 + e}))
                 r |= 1u << j;
             }
-            if (!p.nfa_seq && r == 0x80u) continue;   // patterns: no state can use it
+            // patterns: no state can use it (tolerant: it may still expire partials)
+            if (!p.nfa_seq && r == 0x80u && !p.tolerant) continue;
             nrole[e] = r;
             const int kc = p.key_col_s[sid[e]];
             if (kc >= 0) key[e] = (int64_t)load_col(a.rows.cols.p[kc], a.rows.cols.t[kc], row0 + e);
@@ -517,8 +519,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
           if (p.g_walk_prog >= 0) {
             role_b = is_b;
           } else {
-            role_b = is_b & eval_run<E, kVm>(p.g_terms, a.vm, p.g_raw_prog, R, a.rows, row0, nvalid);
-            role_g = role_b;
+            role_g = is_b & eval_run<E, kVm>(p.g_terms, a.vm, p.g_raw_prog, R, a.rows, row0, nvalid);
+            role_b = p.tolerant ? is_b : role_g;
           }
         }
 #pragma unroll
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(PartArgs a) {
       uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
                       ((role_g >> e) & 1u) * ROLE_G;
       if constexpr (kVm) {
-        if (p.nfa_mode) role = nrole[e];
+        if (p.nfa_mode && !p.nfa_pair) role = nrole[e];
       }
       if (!role) continue;
       const int64_t kfield = shard_key(key[e], p.key_stride, p.key_offset);
@@ -1192,7 +1194,7 @@ __device__ uint32_t walk_key(const WalkArgs& a, WalkLds& L, uint64_t* R, int key
     }
     if ((role & ROLE_A) && (p.every || !started)) {
       started = true;
-      if (p.within >= 0) {
+      if (p.within >= 0 && !p.tolerant) {
         // event-time order: partials older than W can never complete again
         int drop = 0;
         while (drop < n && ts - entry_ts(PL(drop)) > p.within) ++drop;
@@ -1383,6 +1385,15 @@ template <bool kVm>
 __device__ __forceinline__ bool nfa_cond(const WalkArgs& a, uint64_t* R, int j, uint32_t role,
                                          const uint64_t* slot, int64_t st, const uint64_t* rec, int64_t ts_base) {
   const PatternArgs& p = a.pat;
+  if (p.nfa_pair) {   // 2-state record roles: A = s1's condition, G = g passed in the partition
+    if (j == 0) return (role & ROLE_A) != 0;
+    if (role & ROLE_G) return true;
+    if (!(role & ROLE_B) || !kVm || p.g_walk_prog < 0) return false;
+    const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, st};
+    bool isnull = false;
+    const uint64_t v = eval_env(a.vm, p.g_walk_prog, R, env, &isnull);
+    return !isnull && (v & 1u);
+  }
   if (!((role >> j) & 1u)) return false;
   if (!kVm || p.st_walk[j] < 0) return true;
   const MatchEnv env{slot, nullptr, p.cap_from_rec, rec, ts_base, st};
@@ -1490,7 +1501,9 @@ __device__ __noinline__ void nfa_key(const WalkArgs& a, WalkLds& L, uint64_t* R,
       int nf = 0;   // advanced partials, staged in slots [CAP, 2 CAP)
       for (int i = 0; i < n; ++i) {
         uint64_t* si = NSLOT(i);
-        const int j = (int)(si[st] & 0xffu);
+        // a 2-state pattern's partials all wait on state 1 (its at-rest slots
+        // do not hold the state word)
+        const int j = p.nfa_pair ? 1 : (int)(si[st] & 0xffu);
         if (p.st_stream[j] != stream) { copy_slot(m++, i); continue; }
         if (p.within >= 0) {
           const int64_t d = ts - (int64_t)si[0];

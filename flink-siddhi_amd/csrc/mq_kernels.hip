@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kMqPartThreads, 1) void k_mqpart(MqPartArgs a) {
   // predecessor of the lane's first row (read by lanes that hold rows only:
   // row0 - 1 of a lane past the batch end would read past the ts column)
   int64_t prev_last = 0;
-  if (valid & 1u) prev_last = row0 > 0 ? a.rows.ts[row0 - 1] : a.rows.prev_ts;
+  if (valid & 1u) prev_last = row0 > 0 ? a.rows.ts[row0 - 1] : batch_prev_ts(a.rows);
 #pragma unroll
   for (int g = 0; g < RPL / EB; ++g) {
     const uint32_t vg = (valid >> (EB * g)) & ((1u << EB) - 1u);

@@ -98,7 +98,7 @@ class cep_options(C.Structure):
                 ("ordered_output", C.c_int32), ("key_stride", C.c_int32),
                 ("key_offset", C.c_int32), ("pending_pool_log2", C.c_int32),
                 ("sparse_keys", C.c_int32), ("late_policy", C.c_int32), ("omit_seq", C.c_int32),
-                ("reserved", C.c_int32 * 3)]
+                ("ts_order", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 class cep_batch(C.Structure):

@@ -458,7 +458,9 @@ class SiddhiAppRuntime:
             return t.clone() if copy else t
 
         ts = wrap(C.cast(r.ts, C.c_void_p).value, "<i8")
-        seq = wrap(C.cast(r.seq, C.c_void_p).value, "<i8")
+        # None under omit_seq with unordered output (the kernels do not write them)
+        seq_ptr = C.cast(r.seq, C.c_void_p).value
+        seq = wrap(seq_ptr, "<i8") if seq_ptr else None
         cols = [wrap(r.cols[c], np.dtype(L.NUMPY_DTYPES[t]).str) for c, t in enumerate(types)]
         return ts, seq, cols
 

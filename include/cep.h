@@ -102,17 +102,39 @@ typedef struct cep_options {
                               assigns up to key_capacity dense slots; values come back
                               unchanged in `select s1.k`); 0: ints in [0, key_capacity) */
   int32_t late_policy;     /* event time (cep_watermark): a row older than rows an earlier
-                              watermark released is a late event.  0: dropped and counted in
-                              cep_stats.late_events (default); 1: dropped, and cep_watermark
-                              returns CEP_E_ARG after releasing the on-time rows.  The
-                              reference hands late rows to Siddhi out of order
-                              (AbstractSiddhiOperator.java:238-245); `within` and sequences
-                              need event-time order, so the engine never processes them. */
+                              watermark released is a late event (counted in
+                              cep_stats.late_events).  2: delivered, as the reference does
+                              (default): it stays buffered and the next watermark releases it
+                              with that watermark's rows in (ts, arrival) order, so the
+                              engine sees a ts below ones it has processed
+                              (AbstractSiddhiOperator.java:222-231 offers every row to the
+                              PriorityQueue, :238-245 drains ts <= mark); `within` then
+                              follows App. A.3's |ts(B) - ts(s1)| > W rule (ts_order 0; with
+                              ts_order 1 a release holding late rows runs the order-tolerant
+                              path against state kept in event-time form).
+                              0: dropped; 1: dropped, and cep_watermark returns CEP_E_ARG
+                              after releasing the on-time rows. */
   int32_t omit_seq;        /* 1: cep_rows.seq is NULL in callbacks and the seq column is not
                               copied to the host (StreamOutputHandler.receive,
                               operator/StreamOutputHandler.java:63-92, never reads it;
                               saves 8 B per delivered row); 0: delivered (default) */
-  int32_t reserved[3];
+  int32_t ts_order;        /* timestamps of the rows a pattern with `within` sees.
+                              0 (default): any order, as the reference accepts (processing
+                              time, late rows delivered by late_policy 2, any caller).  Such
+                              patterns run the order-tolerant path: every row of the stream
+                              a partial waits on is kept, and a partial is dropped exactly
+                              when SURVEY App. A.3 drops it (|ts(event) - ts(s1)| > W, on
+                              events of that stream), so the state and every match equal the
+                              oracle's for any order.
+                              1: the caller guarantees non-decreasing ts (event-time order,
+                              e.g. a watermark drain with late_policy 0): the event-time fast
+                              paths (closed form, predicate push-down of B's, pruning at A
+                              arrivals, hot keys), several times faster; a descent fails the
+                              next cep_flush with CEP_E_ARG.  Sequences and multi-query groups
+                              prune by |ts - ts(s1)| in any order either way (ts_order 1
+                              only adds the check); the multi-GPU record / row shuffles
+                              always run the event-time paths. */
+  int32_t reserved[2];
 } cep_options;
 
 /* Fill *opt with defaults. */

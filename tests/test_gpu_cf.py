@@ -58,7 +58,7 @@ def check_path(rt, path):
 
 
 def run(plan, w, path, batches=1, device=False, **opts):
-    rt = fs.SiddhiAppRuntime(plan, **opts)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, **opts)
     rt.add_callback("O")
     send_all(rt, w, batches, device)
     got = engine_rows(rt.collect("O"))
@@ -148,7 +148,7 @@ def test_snapshot_cf_restore_general(monkeypatch):
     first_w = {k: v[:half] for k, v in w.items()}
     second_w = {k: v[half:] for k, v in w.items()}
     monkeypatch.delenv("CEP_NO_CF", raising=False)
-    rt = fs.SiddhiAppRuntime(plan)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1)
     rt.add_callback("O")
     send_all(rt, first_w)
     first = engine_rows(rt.collect("O"))
@@ -156,7 +156,7 @@ def test_snapshot_cf_restore_general(monkeypatch):
     snap = rt.snapshot()
     rt.shutdown()
     monkeypatch.setenv("CEP_NO_CF", "1")
-    rt2 = fs.SiddhiAppRuntime(plan)
+    rt2 = fs.SiddhiAppRuntime(plan, ts_order=1)
     rt2.add_callback("O")
     rt2.restore(snap)
     send_all(rt2, second_w)
@@ -175,7 +175,7 @@ def test_pending_lists_longer_than_pending_slots(path):
     w = workload.generate(0, 60000, 64, rate=1)
     plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id % 25 == 0")
     if path == "general":
-        rt = fs.SiddhiAppRuntime(plan, pending_slots=16)
+        rt = fs.SiddhiAppRuntime(plan, ts_order=1, pending_slots=16)
         rt.add_callback("O")
         rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
         with pytest.raises(fs.CepCapacityError):
@@ -188,7 +188,7 @@ def test_pending_lists_longer_than_pending_slots(path):
 def test_pending_pool_exhausted_is_reported():
     w = workload.generate(0, 30000, 64, rate=1)
     plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id == 1000")   # no B: lists only grow
-    rt = fs.SiddhiAppRuntime(plan, pending_slots=4, pending_pool_log2=6)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, pending_slots=4, pending_pool_log2=6)
     rt.add_callback("O")
     rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
     with pytest.raises(fs.CepCapacityError, match="pool"):
@@ -203,13 +203,13 @@ def test_overflow_snapshot_restore():
     plan = workload.PATTERN_PLAN.replace("id % 7 == 0", "id % 25 == 0")
     want = oracle_run(plan, workload_events(w)).get("O", [])
     h = 31000
-    rt = fs.SiddhiAppRuntime(plan, pending_slots=4)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, pending_slots=4)
     rt.add_callback("O")
     send_all(rt, {k: v[:h] for k, v in w.items()})
     first = engine_rows(rt.collect("O"))
     snap = rt.snapshot()
     rt.shutdown()
-    rt2 = fs.SiddhiAppRuntime(plan, pending_slots=4)
+    rt2 = fs.SiddhiAppRuntime(plan, ts_order=1, pending_slots=4)
     rt2.add_callback("O")
     rt2.restore(snap)
     send_all(rt2, {k: v[h:] for k, v in w.items()})
@@ -223,7 +223,7 @@ def test_fast_path_engaged_on_config3_device_batch():
     os.environ.pop("CEP_NO_CF", None)
     d = workload.generate_device(0, 1 << 20, 1 << 14, rate=8)
     torch.cuda.synchronize()
-    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, ts_order=1)
     rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
     rt.flush()
     st = rt.stats()

@@ -35,7 +35,7 @@ def run_engine(sizes, keys=K, rate=R, plan=workload.PATTERN_PLAN, key_of=None, *
     """Device batches of the config-3 stream through the engine; returns the
     concatenated device output as numpy (emission order) and the stats."""
     import torch
-    rt = fs.SiddhiAppRuntime(plan, chunk_events=CHUNK, ordered_output=0, **opts)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, chunk_events=CHUNK, ordered_output=0, **opts)
     first, parts = 0, []
     for n in sizes:
         d = workload.generate_device(first, n, keys, rate=rate)
@@ -103,7 +103,7 @@ def test_vm_walk_16mi_chunks_vs_oracle():
     import torch
     plan = workload.PATTERN_PLAN.replace("s1.price as p1", "s1.price * 2.0 as p1")
     n = (1 << 24) + 123457
-    rt = fs.SiddhiAppRuntime(plan, chunk_events=1 << 24, ordered_output=0)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, chunk_events=1 << 24, ordered_output=0)
     d = workload.generate_device(0, n, K, rate=R)
     rt.send("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], streams=d["stream"])
     ts, seq, cols = rt.output_tensors("O")
@@ -127,7 +127,7 @@ def test_config3_ordered_delivery_bench_geometry():
     # row identical to the oracle's, in the same position.
     import torch
     sizes = [CHUNK + 777, 1 << 23]
-    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, chunk_events=CHUNK, ordered_output=1)
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, ts_order=1, chunk_events=CHUNK, ordered_output=1)
     rt.add_callback("O")
     first = 0
     for n in sizes:

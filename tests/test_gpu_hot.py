@@ -23,7 +23,7 @@ from test_gpu_geometry import F, assert_same_per_key  # noqa: E402
 def run_batches(batches, keys, rate, plan, chunk, key_value=None, **opts):
     """batches: [(first, n, key remap table or None)] -> (device rows as numpy, stats)."""
     import torch
-    rt = fs.SiddhiAppRuntime(plan, chunk_events=chunk, ordered_output=0, key_capacity=keys, **opts)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, chunk_events=chunk, ordered_output=0, key_capacity=keys, **opts)
     parts = []
     for first, n, table in batches:
         d = workload.generate_device(first, n, keys, rate=rate)
@@ -126,7 +126,7 @@ def test_hot_keys_on_shuffle_owners(world):
     keys, rate, n_per, steps = 1 << 16, 400, 1 << 20, 4
     z = torch.from_numpy(workload.zipf_map(keys, seed=5)).cuda()
     plan = workload.PATTERN_PLAN
-    rts = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=1 << 20,
+    rts = [fs.SiddhiAppRuntime(plan, ts_order=1, key_stride=world, key_offset=r, chunk_events=1 << 20,
                                key_capacity=keys, ordered_output=0) for r in range(world)]
     parts = [[] for _ in range(world)]
     for s in range(steps):

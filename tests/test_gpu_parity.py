@@ -241,16 +241,6 @@ def test_disabled_runtime_drops_events():
     assert len(rt.collect("O")) == 0
 
 
-def test_out_of_order_within_is_reported():
-    w = workload.generate(0, 5000, 16, rate=1)
-    w["ts"] = w["ts"][::-1].copy()
-    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
-    rt.add_callback("O")
-    rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
-    with pytest.raises(ValueError):
-        rt.flush()
-
-
 def test_device_resident_batch_matches_host_batch():
     import torch
     n, keys = 50000, 8192

@@ -30,8 +30,8 @@ def test_route_exchange_matches_oracle(world, path, monkeypatch):
         monkeypatch.delenv("CEP_NO_CF", raising=False)
     n_per, keys = 12000, 600
     plan = workload.PATTERN_PLAN
-    sender = fs.SiddhiAppRuntime(plan)
-    owners = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=8192)
+    sender = fs.SiddhiAppRuntime(plan, ts_order=1)
+    owners = [fs.SiddhiAppRuntime(plan, ts_order=1, key_stride=world, key_offset=r, chunk_events=8192)
               for r in range(world)]
     for o in owners:
         o.add_callback("O")
@@ -79,7 +79,7 @@ def test_fast_route_equals_general_route(world, monkeypatch):
             monkeypatch.setenv("CEP_NO_CF", "1")
         else:
             monkeypatch.delenv("CEP_NO_CF", raising=False)
-        rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+        rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, ts_order=1)
         recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
                                 seq0=7, streams=d["stream"])
         got[path] = (recs[:sum(counts)].cpu().numpy().copy(), counts)
@@ -99,7 +99,7 @@ def test_pipelined_route_overlaps_walk(world):
     # reuse ordered by guard streams (send_records(signal=False) + signal)
     steps, n_per, keys = 4, 40000, 2000
     plan = workload.PATTERN_PLAN
-    rts = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=16384)
+    rts = [fs.SiddhiAppRuntime(plan, ts_order=1, key_stride=world, key_offset=r, chunk_events=16384)
            for r in range(world)]
     for rt in rts:
         rt.add_callback("O")
@@ -157,8 +157,8 @@ def _padded_round(world, n_per, keys, seg_cap, steps=1, cap_fn=None):
     of every source in source order (the equal-split all-to-all) and feeds
     them to cep_send_records_padded.  No counts are read back anywhere."""
     plan = workload.PATTERN_PLAN
-    senders = [fs.SiddhiAppRuntime(plan) for _ in range(world)]
-    owners = [fs.SiddhiAppRuntime(plan, key_stride=world, key_offset=r, chunk_events=8192)
+    senders = [fs.SiddhiAppRuntime(plan, ts_order=1) for _ in range(world)]
+    owners = [fs.SiddhiAppRuntime(plan, ts_order=1, key_stride=world, key_offset=r, chunk_events=8192)
               for r in range(world)]
     for o in owners:
         o.add_callback("O")
@@ -209,7 +209,7 @@ def test_padded_segment_headers_carry_the_counts():
     world, n, keys = 4, 30000, 900
     w = workload.generate(0, n, keys, rate=1)
     d = _dev(w)
-    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN)
+    rt = fs.SiddhiAppRuntime(workload.PATTERN_PLAN, ts_order=1)
     recs, counts = rt.route("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world, seq0=5,
                             streams=d["stream"])
     recs = recs[:sum(counts)].cpu().numpy().copy()

@@ -20,7 +20,7 @@ LONG_PLAN = workload.PATTERN_PLAN.replace("(k int,", "(k long,")
 
 
 def run(plan, w, batches=2, device=False, **opts):
-    rt = fs.SiddhiAppRuntime(plan, sparse_keys=1, **opts)
+    rt = fs.SiddhiAppRuntime(plan, ts_order=1, sparse_keys=1, **opts)
     rt.add_callback("O")
     n = len(w["ts"])
     cuts = np.linspace(0, n, batches + 1).astype(int)
@@ -76,7 +76,7 @@ def test_int_keys_outside_key_capacity():
 def test_more_values_than_key_capacity_is_reported():
     w = workload.generate(0, 20000, 3000, rate=1)
     w["k"] = long_values(3000, 6)[w["k"]]
-    rt = fs.SiddhiAppRuntime(LONG_PLAN, sparse_keys=1, key_capacity=1024)
+    rt = fs.SiddhiAppRuntime(LONG_PLAN, ts_order=1, sparse_keys=1, key_capacity=1024)
     rt.add_callback("O")
     rt.send("A", w["ts"], [w["k"], w["ts"], w["id"], w["price"]], streams=w["stream"])
     with pytest.raises(fs.CepCapacityError, match="distinct"):
@@ -92,7 +92,7 @@ def test_sparse_key_map_survives_snapshot():
     rt, first = run(LONG_PLAN, {c: v[:h] for c, v in w.items()}, batches=1, key_capacity=4096)
     snap = rt.snapshot()
     rt.shutdown()
-    rt2 = fs.SiddhiAppRuntime(LONG_PLAN, sparse_keys=1, key_capacity=4096)
+    rt2 = fs.SiddhiAppRuntime(LONG_PLAN, ts_order=1, sparse_keys=1, key_capacity=4096)
     rt2.add_callback("O")
     rt2.restore(snap)
     rt2.send("A", w["ts"][h:], [w["k"][h:], w["ts"][h:], w["id"][h:], w["price"][h:]], streams=w["stream"][h:])
@@ -105,4 +105,4 @@ def test_sparse_key_map_survives_snapshot():
 def test_key_in_a_filter_is_unsupported():
     plan = workload.PATTERN_PLAN.replace("A[price > 0.5]", "A[price > 0.5 and k > 3]")
     with pytest.raises(fs.UnsupportedPlanException):
-        fs.SiddhiAppRuntime(plan, sparse_keys=1)
+        fs.SiddhiAppRuntime(plan, ts_order=1, sparse_keys=1)
