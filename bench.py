@@ -488,9 +488,11 @@ def main():
         del w
     if args.ordered:
         opts["ordered_output"] = 1
-    if args.deliver and not args.with_seq:
+    if not args.with_seq:
         # the reference's StreamOutputHandler never reads the arrival number:
-        # it is not gathered or copied to the host (cep_options.omit_seq)
+        # with unordered output it is not even stored, and it is not gathered
+        # or copied to the host (cep_options.omit_seq); the parity runs above
+        # keep it (their digests cover it)
         opts["omit_seq"] = 1
     rt = fs.SiddhiAppRuntime(plan, **opts)
 

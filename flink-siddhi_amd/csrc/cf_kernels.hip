@@ -565,7 +565,7 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
     store_col(a.out.col[c], a.out.type[c], (int64_t)pos, v);
   }
   a.out.ts[pos] = bts;
-  a.out.seq[pos] = seq;
+  if (a.out.write_seq) a.out.seq[pos] = seq;
 }
 
 }  // namespace

@@ -100,6 +100,7 @@ struct OutStream {
   unsigned long long* count = nullptr;   // device cursor
   int64_t cap = 0;                       // allocated rows
   int64_t bound = 0;                     // upper bound of rows since last flush
+  bool write_seq = true;                 // the kernels store arrival numbers (someone reads them)
   cep_emit_fn fn = nullptr;
   void* user = nullptr;
   // pinned host copies for callback delivery (D2H at PCIe speed)
@@ -346,6 +347,7 @@ OutArgs out_args(OutStream& o, const Query& q) {
   oa.seq = (int64_t*)o.seq.p;
   oa.count = o.count;
   oa.cap = o.cap;
+  oa.write_seq = o.write_seq ? 1 : 0;
   return oa;
 }
 
@@ -943,6 +945,9 @@ int create_runtime(cep_app* a) {
     for (auto& at : sd.attrs) o.types.push_back(at.type);
     o.cols.resize(sd.attrs.size());
     o.count = (unsigned long long*)a->out_counts.p + a->outs.size();
+    // arrival numbers: read by the ordered flush and by consumers that asked
+    // for them (cep_output_device returns seq = NULL otherwise)
+    o.write_seq = !(a->opt.omit_seq && !a->opt.ordered_output);
     a->outs.push_back(std::move(o));
   }
   {
@@ -1292,8 +1297,6 @@ int run_filter(cep_app* a, const Query& q, const RowsArgs& rows) {
       fc = al(rows.cols.p[fa.pcol[k]], type_width(rows.cols.t[fa.pcol[k]]));
     if (fc && rows.stream) fc = al(rows.stream, 1);
   }
-  // arrival numbers are written only when someone reads them
-  fa.write_seq = (a->opt.omit_seq && !a->opt.ordered_output) ? 0 : 1;
   LaunchTimer t(a, CEP_K_FILTER);
   if (fc) {
     const int64_t tr = filterc_rows_per_tile();
@@ -1748,13 +1751,14 @@ int run_mq(cep_app* a, MqRT& g, const RowsArgs& rows_all) {
     const int rc = ensure_out_cap(a, o, o.bound);
     if (rc) return rc;
     MqQuery& d = g.hq[i];
-    bool same = d.out_ts == (int64_t*)o.ts.p && d.out_seq == (int64_t*)o.seq.p && d.out_count == o.count &&
+    int64_t* oseq = o.write_seq ? (int64_t*)o.seq.p : nullptr;   // not read: not stored
+    bool same = d.out_ts == (int64_t*)o.ts.p && d.out_seq == oseq && d.out_count == o.count &&
                 d.out_cap == o.cap;
     for (int c = 0; c < d.nsel; ++c) same = same && d.out_col[c] == o.cols[c].p;
     if (!same) {
       for (int c = 0; c < d.nsel; ++c) d.out_col[c] = o.cols[c].p;
       d.out_ts = (int64_t*)o.ts.p;
-      d.out_seq = (int64_t*)o.seq.p;
+      d.out_seq = oseq;
       d.out_count = o.count;
       d.out_cap = o.cap;
       g.dq_dirty = true;

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kFcThreads, FC_MINW) void k_filterc(FilterArgs a) {
           store_col(a.out.col[c], a.out.type[c], pos, load_col(a.rows.cols.p[col], a.rows.cols.t[col], row));
         }
         a.out.ts[pos] = vts;
-        if (a.write_seq) a.out.seq[pos] = vseq;
+        if (a.out.write_seq) a.out.seq[pos] = vseq;
       }
     }
   }

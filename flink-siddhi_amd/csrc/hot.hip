@@ -97,7 +97,7 @@ __device__ __forceinline__ void hot_emit_row(const HotArgs& a, unsigned long lon
     store_col(a.out.col[c], a.out.type[c], (int64_t)pos, v);
   }
   a.out.ts[pos] = bts;
-  a.out.seq[pos] = seq;
+  if (a.out.write_seq) a.out.seq[pos] = seq;
 }
 
 // A record's logical captures (cap_phys: -1 = its event ts).

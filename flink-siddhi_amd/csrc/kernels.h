@@ -55,6 +55,7 @@ struct OutArgs {
   int64_t* seq;
   unsigned long long* count;   // rows written so far (atomic cursor)
   int64_t cap;
+  int32_t write_seq;           // 0: nobody reads the arrival numbers (omit_seq, unordered output)
 };
 
 // Error flags (device word, OR-ed).
@@ -92,7 +93,6 @@ struct FilterArgs {
   int32_t npref;
   int32_t pcol[kPref];
   int32_t fslot[kMaxTerms];
-  int32_t write_seq;       // 0: the output's arrival numbers are not needed (omit_seq, unordered)
 };
 
 // ------------------------------------------------------- keyed pattern --

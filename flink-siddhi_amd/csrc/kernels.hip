@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kFilterThreads) void k_filter(FilterArgs a) {
         store_col(a.out.col[c], a.out.type[c], pos, v);
       }
       a.out.ts[pos] = a.rows.ts[row];
-      a.out.seq[pos] = row_seq(a.rows, row);
+      if (a.out.write_seq) a.out.seq[pos] = row_seq(a.rows, row);
     }
     ++pos;
   }
@@ -1116,7 +1116,7 @@ __device__ __forceinline__ void emit_row(const WalkArgs& a, uint64_t* R, const E
     store_col(a.out.col[c], a.out.type[c], (int64_t)pos, v);
   }
   a.out.ts[pos] = env.ts();
-  a.out.seq[pos] = seq;
+  if (a.out.write_seq) a.out.seq[pos] = seq;
 }
 
 // Original key value of dense key kl (shard ownership: key = kl*stride + offset).

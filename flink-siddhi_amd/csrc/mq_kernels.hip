@@ -334,7 +334,7 @@ __device__ __forceinline__ void mq_store_row(const MqHot& H, int nsel, unsigned 
     else ((g8*)(uintptr_t)H.col[x])[p] = (uint8_t)(v & 1u);
   }
   ((g64*)(uintptr_t)H.ts)[p] = (uint64_t)ts;
-  ((g64*)(uintptr_t)H.seq)[p] = (uint64_t)seq;
+  if (H.seq) ((g64*)(uintptr_t)H.seq)[p] = (uint64_t)seq;   // 0: nobody reads them
 }
 
 // One sequence query over a block of 64 keys (lane = key): restates
@@ -891,7 +891,7 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
       }
       const uint32_t row = mq_row(w0);
       ((g64*)Q.out_ts)[p] = (uint64_t)ts;
-      ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
+      if (Q.out_seq) ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
     }
     wave_lds_sync();
     curv[i] += sc[i];
@@ -986,7 +986,7 @@ __device__ __forceinline__ void mq_agg_fast(const MqLds<NC>& L, const MqCtx<NC>&
               else ((g8*)Q.out_col[x])[p] = (uint8_t)(v & 1u);
             }
             ((g64*)Q.out_ts)[p] = (uint64_t)ts;
-            ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
+            if (Q.out_seq) ((g64*)Q.out_seq)[p] = (uint64_t)(c.in_seq ? c.in_seq[row] : c.seq_base + row);
           }
           curv[i] += n;
         } else if (em && !(c.ablate & 2)) {
