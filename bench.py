@@ -549,26 +549,24 @@ def main():
 
     seg_cap = [0]
 
+    pshuf = [None]
+
     def run_padded(blist):
-        # Padded exchange (keyed pattern records): fixed owner segments with
-        # in-band counts, one equal-split all-to-all, nothing read back — the
-        # step loop has no host round trip.  route_padded(wait=True) orders
-        # the route of step s+1 after torch's stream, i.e. after the
-        # all-to-all that last read its send buffer; the walk of step s keeps
-        # running on the engine stream.
+        # Padded exchange with a spill (flink_siddhi.shuffle.PaddedShuffle):
+        # fixed owner segments with in-band counts, one equal-split
+        # all-to-all, nothing read back on the step's critical path; an
+        # owner's records past seg_cap go to a spill buffer and, when any
+        # rank spilled (one host all-reduce of an integer, one step late),
+        # through a second exact exchange -- a key-distribution shift never
+        # drops a record.  The owner's walk of step s is queued at step s+1.
         from flink_siddhi import shuffle
-        cap = seg_cap[0]
-        for i, d in enumerate(blist):
-            j = i % 2
-            segs = rt.route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], world,
-                                   seq0=d["first"], seg_cap=cap, streams=d["stream"],
-                                   out=bufs.get(("psend", j)), rows=not pattern)
-            bufs[("psend", j)] = segs
-            torch.cuda.current_stream().wait_stream(guard[j])   # the walk that last read precv[j]
-            recv = shuffle.exchange_padded(segs, world, out=bufs.get(("precv", j)))
-            bufs[("precv", j)] = recv
-            rt.send_padded(recv, world, cap, n, signal=False, rows=not pattern)
-            rt.signal(guard[j])
+        if pshuf[0] is None:
+            pshuf[0] = shuffle.PaddedShuffle(rt, world, seg_cap[0], spill_cap=n // 2, rows=not pattern)
+        ps = pshuf[0]
+        for d in blist:
+            ps.step("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]], seq0=d["first"], events=n,
+                    streams=d["stream"])
+        ps.finish()
         rt.flush()
 
     def run_shuffle(blist):
@@ -735,7 +733,8 @@ def main():
                                      else "any order (ts_order=0: order-tolerant path)"),
                         "ingest": (("%s all-to-all key shuffle (%s)" % ("rccl" if _coll_device() == "cuda"
                                                                          else "gloo host-staged",
-                                                                         "padded segments, in-band counts"
+                                                                         "padded segments, in-band counts, "
+                                                                         "spill exchange on overflow"
                                                                          if args.exchange == "padded"
                                                                          else "two-phase"))
                                     if shuffle_mode else
@@ -758,6 +757,7 @@ def main():
                        if config5 else
                        {"workload": "config2: inputStream[price > 0.5 and id % 7 == 0] select *",
                         "events_per_step_per_gpu": n, "parallelism": "replicas x%d" % world}),
+            "shuffle_spilled_steps": pshuf[0].spilled_steps if pshuf[0] is not None else None,
             "matches_per_s": round(matches_total / dt_max, 1),
             "matches_per_event": round(m_per_event, 5),
             "pipeline_roofline": pipeline,

@@ -3125,8 +3125,14 @@ int cep_record_words(cep_app* a) {
 // seg_cap == 0: owner-contiguous output, counts read back (cep_route_batch);
 // seg_cap > 0: padded owner segments with in-band counts, nothing read back
 // (cep_route_batch_padded).
+struct SpillArgs {
+  void* out = nullptr;         // nullptr: records past seg_cap are dropped (and flagged)
+  int64_t cap = 0;             // records the spill holds
+  int64_t* counts = nullptr;   // device: spilled records per owner
+};
+
 static int route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out,
-                       int64_t rec_cap, int64_t* counts_host, int64_t seg_cap) {
+                       int64_t rec_cap, int64_t* counts_host, int64_t seg_cap, const SpillArgs& sp = SpillArgs()) {
   if (!a || !b || world <= 0 || (seg_cap == 0 && !counts_host) || seg_cap < 0) return CEP_E_ARG;
   if (world > kMaxWorld) return fail(a, CEP_E_ARG, "world exceeds " + std::to_string(kMaxWorld));
   if (a->pats.size() != 1 || a->app.queries.size() != 1)
@@ -3183,6 +3189,9 @@ static int route_batch(cep_app* a, const cep_batch* b, int world, int64_t seq0, 
   ra.tcount = (uint32_t*)a->route_tcount.p;
   ra.err = (unsigned int*)a->rerr.p;
   ra.seg_cap = seg_cap;
+  ra.spill = (uint64_t*)sp.out;
+  ra.spill_cap = sp.cap;
+  ra.spill_counts = sp.counts;
   {
     LaunchTimer t(a, CEP_K_ROUTE, rs);
     if (fast) {
@@ -3254,6 +3263,17 @@ int cep_route_batch_padded(cep_app* a, const cep_batch* b, int world, int64_t se
                            int64_t seg_out_cap, int64_t seg_cap) {
   if (seg_cap <= 0) return CEP_E_ARG;
   return route_join_host(a, b, route_batch(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap));
+}
+
+int cep_route_batch_padded_spill(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* seg_out,
+                                 int64_t seg_out_cap, int64_t seg_cap, void* spill_out, int64_t spill_cap,
+                                 int64_t* spill_counts) {
+  if (seg_cap <= 0 || !spill_out || spill_cap < 0 || !spill_counts) return CEP_E_ARG;
+  SpillArgs sp;
+  sp.out = spill_out;
+  sp.cap = spill_cap;
+  sp.counts = spill_counts;
+  return route_join_host(a, b, route_batch(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap, sp));
 }
 
 // Row shuffle plan: per input handle the owner key column (-1: any owner,
@@ -3363,7 +3383,7 @@ int cep_row_words(cep_app* a) {
 // seg_cap == 0: owner-contiguous rows, counts read back (cep_route_rows);
 // seg_cap > 0: padded owner segments, counts in-band (cep_route_rows_padded).
 static int route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* rec_out, int64_t rec_cap,
-                      int64_t* counts_host, int64_t seg_cap) {
+                      int64_t* counts_host, int64_t seg_cap, const SpillArgs& sp = SpillArgs()) {
   if (!a || !b || world <= 0 || seg_cap < 0 || (seg_cap == 0 && !counts_host)) return CEP_E_ARG;
   if (world > kMaxWorld) return fail(a, CEP_E_ARG, "world exceeds " + std::to_string(kMaxWorld));
   int32_t kc[8];
@@ -3414,6 +3434,9 @@ static int route_rows(cep_app* a, const cep_batch* b, int world, int64_t seq0, v
   ra.tcount = (uint32_t*)a->route_tcount.p;
   ra.err = (unsigned int*)a->rerr.p;
   ra.seg_cap = seg_cap;
+  ra.spill = (uint64_t*)sp.out;
+  ra.spill_cap = sp.cap;
+  ra.spill_counts = sp.counts;
   {
     LaunchTimer t(a, CEP_K_ROUTE, rs);
     launch_route_rows(ra, ntiles, (uint32_t*)a->route_toffs.p, (unsigned long long*)a->route_dcount.p,
@@ -3454,6 +3477,17 @@ int cep_route_rows_padded(cep_app* a, const cep_batch* b, int world, int64_t seq
                           int64_t seg_out_cap, int64_t seg_cap) {
   if (seg_cap <= 0) return CEP_E_ARG;
   return route_join_host(a, b, route_rows(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap));
+}
+
+int cep_route_rows_padded_spill(cep_app* a, const cep_batch* b, int world, int64_t seq0, void* seg_out,
+                                int64_t seg_out_cap, int64_t seg_cap, void* spill_out, int64_t spill_cap,
+                                int64_t* spill_counts) {
+  if (seg_cap <= 0 || !spill_out || spill_cap < 0 || !spill_counts) return CEP_E_ARG;
+  SpillArgs sp;
+  sp.out = spill_out;
+  sp.cap = spill_cap;
+  sp.counts = spill_counts;
+  return route_join_host(a, b, route_rows(a, b, world, seq0, seg_out, seg_out_cap, nullptr, seg_cap, sp));
 }
 
 int cep_send_rows_padded(cep_app* a, const void* segs, int world, int64_t seg_cap, int64_t events_represented) {

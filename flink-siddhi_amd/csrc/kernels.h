@@ -195,6 +195,9 @@ struct RowRouteArgs {
   uint32_t* tcount;            // [ntiles][world]
   unsigned int* err;
   int64_t seg_cap;             // > 0: padded owner segments (cep_route_rows_padded)
+  uint64_t* spill;             // see RouteArgs
+  int64_t spill_cap;
+  int64_t* spill_counts;
 };
 
 // Stream handle of the padded row shuffle's header and null rows: no input
@@ -227,6 +230,12 @@ struct RouteArgs {
   // out + (d * (1 + seg_cap) + 1) * wrw, at most seg_cap of them
   int64_t seg_cap;
   int32_t row_mode;            // padded segments of whole rows (cep_route_rows_padded)
+  // padded with spill (cep_route_*_padded_spill): owner d's records past
+  // seg_cap go to spill (owner-grouped, arrival order, at most spill_cap
+  // records in all) and spill_counts[d] gets their number
+  uint64_t* spill;
+  int64_t spill_cap;
+  int64_t* spill_counts;
 };
 
 struct WalkArgs {

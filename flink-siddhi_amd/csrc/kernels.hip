@@ -869,6 +869,9 @@ void launch_route_rows(const RowRouteArgs& a, int64_t ntiles, uint32_t* toffs,
   ra.err = a.err;
   ra.seg_cap = a.seg_cap;
   ra.row_mode = 1;
+  ra.spill = a.spill;
+  ra.spill_cap = a.spill_cap;
+  ra.spill_counts = a.spill_counts;
   launch_route_collect(ra, ntiles, toffs, dcount, out, s);
   if (a.seg_cap > 0) launch_route_pad(ra, dcount, out, s);
 }
@@ -906,6 +909,7 @@ __global__ __launch_bounds__(256) void k_route_gather(RouteArgs a, int64_t ntile
   const int64_t t = blockIdx.x;
   const int wrw = a.wrw;
   unsigned long long obase = 0;
+  int64_t sbase = 0;   // spill: records past seg_cap of the owners before d
   uint32_t src = 0;
   for (int d = 0; d < a.world; ++d) {
     const uint32_t c = a.tcount[t * a.world + d];
@@ -913,9 +917,20 @@ __global__ __launch_bounds__(256) void k_route_gather(RouteArgs a, int64_t ntile
     const uint32_t to = toffs[(int64_t)d * ntiles + t];
     int64_t n = c;
     uint64_t* o;
-    if (a.seg_cap > 0) {   // padded: owner d's segment, records past seg_cap dropped (flagged by k_route_pad)
+    if (a.seg_cap > 0) {   // padded: owner d's segment, records past seg_cap spilled or dropped (k_route_pad flags them)
       n = (int64_t)to >= a.seg_cap ? 0 : (c < a.seg_cap - (int64_t)to ? (int64_t)c : a.seg_cap - (int64_t)to);
       o = out + ((int64_t)d * (1 + a.seg_cap) + 1 + to) * wrw;
+      if (a.spill && n < (int64_t)c) {
+        // the rest of this tile's run: spill slots (to + n - seg_cap) on
+        const int64_t k0 = sbase + (int64_t)to + n - a.seg_cap;
+        const int64_t m = (int64_t)c - n;
+        const int64_t fit = k0 >= a.spill_cap ? 0 : (m < a.spill_cap - k0 ? m : a.spill_cap - k0);
+        uint64_t* so = a.spill + k0 * wrw;
+        const uint64_t* ss = s + n * wrw;
+        for (int64_t w = threadIdx.x; w < fit * wrw; w += blockDim.x) so[w] = ss[w];
+      }
+      const int64_t tot = (int64_t)dcount[d];
+      sbase += tot > a.seg_cap ? tot - a.seg_cap : 0;
     } else {
       o = out + (int64_t)(obase + to) * wrw;
     }
@@ -941,6 +956,17 @@ __global__ __launch_bounds__(256) void k_route_pad(RouteArgs a, const unsigned l
   const int64_t r0 = a.rows.row0, r1 = a.rows.row0 + a.rows.n - 1;
   uint64_t* seg = out + (int64_t)d * (1 + a.seg_cap) * wrw;
   const uint64_t ovf = (int64_t)cnt > a.seg_cap ? 1ull << 63 : 0ull;
+  if (a.spill_counts && blockIdx.x == 0 && threadIdx.x == 0) {
+    // records past seg_cap, all of them in the spill unless it ran out
+    int64_t before = 0;
+    for (int e = 0; e < d; ++e) {
+      const int64_t c = (int64_t)dcount[e];
+      before += c > a.seg_cap ? c - a.seg_cap : 0;
+    }
+    const int64_t over = (int64_t)cnt > a.seg_cap ? (int64_t)cnt - a.seg_cap : 0;
+    a.spill_counts[d] = over;
+    if (before + over > a.spill_cap) set_err(a.err, ERR_SHUFFLE_CAP);
+  }
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)wrw) {
     const unsigned int e = *(volatile unsigned int*)a.err;
     uint64_t h = 0;

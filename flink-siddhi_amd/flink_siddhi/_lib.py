@@ -166,6 +166,12 @@ SIGNATURES = {
     "cep_route_rows_padded": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
                                         C.c_void_p, C.c_int64, C.c_int64]),
     "cep_send_rows_padded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_int64]),
+    "cep_route_batch_padded_spill": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
+                                               C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                               C.c_void_p]),
+    "cep_route_rows_padded_spill": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
+                                              C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                              C.c_void_p]),
     "cep_row_words": (C.c_int, [C.c_void_p]),
     "cep_route_rows": (C.c_int, [C.c_void_p, C.POINTER(cep_batch), C.c_int, C.c_int64,
                                  C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),

@@ -293,12 +293,17 @@ class SiddhiAppRuntime:
         return out, [int(c) for c in counts]
 
     def route_padded(self, stream_id: str, ts, cols: Sequence, world: int, seq0: int, seg_cap: int,
-                     streams=None, out=None, wait: bool = True, rows: bool = False):
+                     streams=None, out=None, wait: bool = True, rows: bool = False, spill=None):
         """Padded sender side (cep_route_batch_padded; rows=True:
         cep_route_rows_padded): a uint64 device tensor [world * (1 + seg_cap),
         words] of fixed owner segments with the counts in-band (segment
         headers).  Nothing is read back: the route is only queued, so the step
-        needs no host round trip."""
+        needs no host round trip.
+
+        spill = (buffer [cap, words], counts [world] int64), device tensors:
+        an owner's records past seg_cap go to the buffer instead of being
+        dropped (cep_route_*_padded_spill; flink_siddhi.shuffle.PaddedShuffle
+        ships them)."""
         import torch
         h = self.input_handle(stream_id)
         defs = self.stream_definition(stream_id)
@@ -322,8 +327,18 @@ class SiddhiAppRuntime:
                         cols=ptrs, on_device=1)
         if wait:
             self._wait_producer(ts)
-        fn = self._lib.cep_route_rows_padded if rows else self._lib.cep_route_batch_padded
-        self._check(fn(self._h, C.byref(b), world, seq0, C.c_void_p(out.data_ptr()), out.shape[0], int(seg_cap)))
+        if spill is None:
+            fn = self._lib.cep_route_rows_padded if rows else self._lib.cep_route_batch_padded
+            self._check(fn(self._h, C.byref(b), world, seq0, C.c_void_p(out.data_ptr()), out.shape[0],
+                           int(seg_cap)))
+        else:
+            sbuf, scnt = spill
+            if sbuf.shape[1] != w or scnt.numel() < world or scnt.dtype != torch.int64:
+                raise ValueError("spill: buffer [cap, %d] and int64 counts [world]" % w)
+            fn = self._lib.cep_route_rows_padded_spill if rows else self._lib.cep_route_batch_padded_spill
+            self._check(fn(self._h, C.byref(b), world, seq0, C.c_void_p(out.data_ptr()), out.shape[0],
+                           int(seg_cap), C.c_void_p(sbuf.data_ptr()), sbuf.shape[0],
+                           C.c_void_p(scnt.data_ptr())))
         # torch's stream (the all-to-all) must not read the segments before the
         # route stream wrote them; the walk queued on the engine stream is not
         # waited for

@@ -133,3 +133,123 @@ def calibrated_capacity(counts: Sequence[int], slack: float = 0.15, floor: int =
         dist.all_reduce(m, op=dist.ReduceOp.MAX, group=g)
     top = int(m.item())
     return int(top + top * slack) + floor
+
+
+def segment_counts(segs: torch.Tensor, world: int, seg_cap: int, rows: bool = False) -> List[int]:
+    """The true per-source record counts in the headers of `world` received
+    padded segments (one small readback): records: header word 0 low 32 bits;
+    rows: bits 32-62 (include/cep.h)."""
+    h = segs.view(world, 1 + seg_cap, -1)[:, 0, 0].cpu()
+    if rows:
+        return [int((int(x) >> 32) & 0x7fffffff) for x in h.tolist()]
+    return [int(int(x) & 0xffffffff) for x in h.tolist()]
+
+
+def merge_padded(recv: torch.Tensor, world: int, seg_cap: int, spill_recv: torch.Tensor,
+                 spill_src_counts: Sequence[int], rows: bool = False) -> torch.Tensor:
+    """Owner input of a step whose padded exchange spilled: per source rank r
+    (in rank order, i.e. global arrival order), the r-th segment's first
+    min(count_r, seg_cap) records then the records r spilled for this owner
+    (spill_recv holds them in source order, spill_src_counts[r] each).  Every
+    record of the step arrives, in the order the owner would have seen them
+    with a large enough seg_cap."""
+    counts = segment_counts(recv, world, seg_cap, rows)
+    segs = recv.view(world, 1 + seg_cap, -1)
+    parts = []
+    off = 0
+    for r in range(world):
+        kept = min(counts[r], seg_cap)
+        if kept:
+            parts.append(segs[r, 1:1 + kept])
+        s = int(spill_src_counts[r])
+        if s:
+            parts.append(spill_recv[off:off + s])
+        off += s
+        if kept + s != counts[r]:
+            raise RuntimeError("padded shuffle: source %d sent %d + %d spilled records for %d routed"
+                               % (r, kept, s, counts[r]))
+    if not parts:
+        return recv[:0].reshape(0, segs.shape[2])
+    return torch.cat(parts, dim=0)
+
+
+class PaddedShuffle:
+    """The padded key shuffle with a spill: no host round trip per step, and
+    no record is ever dropped when an owner's share outgrows seg_cap (VERDICT
+    r04 item 6: a key-distribution shift must not abort the job).
+
+    Step s: route (cep_route_*_padded_spill: records past seg_cap go to a
+    spill buffer, their per-owner counts to a device array copied to pinned
+    memory without a sync), one equal-split all-to-all of the segments.  The
+    owner's walk of step s is queued at step s + 1, after this rank has read
+    its spill counts of step s (long done by then) and all ranks agreed on
+    whether anyone spilled (one host all-reduce of an integer, beside the
+    collectives).  Nobody spilled: the segments go to the engine as they are
+    (cep_send_*_padded).  Someone spilled: one exact exchange of the spill
+    buffers (counts first) and the owner's input is merged per source rank
+    (merge_padded), so every record arrives in global arrival order."""
+
+    def __init__(self, rt, world: int, seg_cap: int, spill_cap: int, rows: bool = False):
+        self.rt, self.world, self.seg_cap, self.spill_cap, self.rows = rt, world, int(seg_cap), int(spill_cap), rows
+        self.words = rt.row_words() if rows else rt.record_words()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.segs = [None, None]
+        self.recv = [None, None]
+        self.merged = [None, None]
+        self.sbuf = [torch.empty((max(1, self.spill_cap), self.words), dtype=torch.int64, device=dev)
+                     for _ in range(2)]
+        self.scnt = [torch.zeros(world, dtype=torch.int64, device=dev) for _ in range(2)]
+        self.shost = [torch.zeros(world, dtype=torch.int64).pin_memory() for _ in range(2)]
+        self.ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.guard = [torch.cuda.Stream(), torch.cuda.Stream()]
+        self.pending = None
+        self.i = 0
+        self.spilled_steps = 0
+        self.spilled_records = 0
+
+    def step(self, stream_id: str, ts, cols, seq0: int, events: int, streams=None):
+        j = self.i % 2
+        self.i += 1
+        rt = self.rt
+        self.segs[j] = rt.route_padded(stream_id, ts, cols, self.world, seq0=seq0, seg_cap=self.seg_cap,
+                                       streams=streams, out=self.segs[j], rows=self.rows,
+                                       spill=(self.sbuf[j], self.scnt[j]))
+        # torch's stream is ordered after the route (route_padded signals it)
+        self.shost[j].copy_(self.scnt[j], non_blocking=True)
+        self.ev[j].record()
+        torch.cuda.current_stream().wait_stream(self.guard[j])   # the walk that last read recv[j]
+        self.recv[j] = exchange_padded(self.segs[j], self.world, out=self.recv[j])
+        if self.pending is not None:
+            self._finish(*self.pending)
+        self.pending = (j, events)
+
+    def finish(self):
+        if self.pending is not None:
+            self._finish(*self.pending)
+            self.pending = None
+
+    def _finish(self, j: int, events: int):
+        self.ev[j].synchronize()
+        local = int(self.shost[j].sum().item())
+        flag = torch.tensor([local], dtype=torch.int64)
+        g = _count_group()
+        if g == "device":
+            flag = flag.cuda()
+            dist.all_reduce(flag)
+        else:
+            dist.all_reduce(flag, group=g)
+        rt = self.rt
+        if int(flag.item()) == 0:
+            rt.send_padded(self.recv[j], self.world, self.seg_cap, events, signal=False, rows=self.rows)
+        else:
+            self.spilled_steps += 1
+            self.spilled_records += local
+            counts = [int(x) for x in self.shost[j].tolist()]
+            spill_recv, m, src = exchange(self.sbuf[j], counts)
+            self.merged[j] = merge_padded(self.recv[j], self.world, self.seg_cap, spill_recv[:m], src, self.rows)
+            n = int(self.merged[j].shape[0])
+            if self.rows:
+                rt.send_rows(self.merged[j], n, events, signal=False)
+            else:
+                rt.send_records(self.merged[j], n, events, signal=False)
+        rt.signal(self.guard[j])

@@ -333,6 +333,22 @@ int cep_route_batch_padded(cep_app* app, const cep_batch* batch, int world,
                            int64_t seg_cap);
 int cep_send_records_padded(cep_app* app, const void* segs, int world,
                             int64_t seg_cap, int64_t events_represented);
+/* As cep_route_batch_padded, but an owner's records past seg_cap are not
+ * lost: they go to spill_out (owner-grouped, each owner's in arrival order,
+ * at most spill_cap records in all) and spill_counts[d] (a device array of
+ * `world` int64, written asynchronously on the route stream) gets their
+ * number.  Nothing is read back.  The caller learns about a spill when it
+ * reads spill_counts (one step later, without stalling the pipeline); then,
+ * instead of cep_send_records_padded, the owner concatenates per source rank
+ * the segment's seg_cap records and that source's spilled records (shipped
+ * in a second, exact exchange) and feeds them with cep_send_records: the
+ * owner's input stays in global arrival order and no record is dropped
+ * (flink_siddhi.shuffle.PaddedShuffle).  Only a spill past spill_cap fails
+ * (CEP_E_CAPACITY at the next flush). */
+int cep_route_batch_padded_spill(cep_app* app, const cep_batch* batch, int world,
+                                 int64_t seq0, void* seg_out, int64_t seg_out_cap,
+                                 int64_t seg_cap, void* spill_out, int64_t spill_cap,
+                                 int64_t* spill_counts);
 /* Make hip_stream wait for the routes queued so far (the route stream only:
  * the all-to-all of step s+1 need not wait for the walk of step s).  A host
  * batch's route runs on the engine stream and is joined into the route
@@ -361,6 +377,11 @@ int cep_send_rows(cep_app* app, const void* recs, int64_t n, int64_t events_repr
  * device and feeds the world segments (source-rank order) as one batch. */
 int cep_route_rows_padded(cep_app* app, const cep_batch* batch, int world, int64_t seq0, void* seg_out,
                           int64_t seg_out_cap, int64_t seg_cap);
+/* Whole rows with a spill, as cep_route_batch_padded_spill (received rows go
+ * to cep_send_rows in the merged order). */
+int cep_route_rows_padded_spill(cep_app* app, const cep_batch* batch, int world, int64_t seq0, void* seg_out,
+                                int64_t seg_out_cap, int64_t seg_cap, void* spill_out, int64_t spill_cap,
+                                int64_t* spill_counts);
 int cep_send_rows_padded(cep_app* app, const void* segs, int world, int64_t seg_cap,
                          int64_t events_represented);
 

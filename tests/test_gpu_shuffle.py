@@ -237,3 +237,81 @@ def test_padded_overflow_fails_the_next_flush():
         owners[0].flush()
     for rt in owners + senders:
         rt.shutdown()
+
+
+def _spill_round(world, n_per, keys, seg_cap, steps, skew_step=None, rows=False):
+    """As _padded_round with cep_route_*_padded_spill: every source's records
+    past seg_cap go to its spill buffer; a step that spilled anywhere reaches
+    the owners merged per source rank (shuffle.merge_padded), the others as
+    padded segments.  skew_step: from that step on most keys map to owner 0
+    (a key-distribution shift mid-stream)."""
+    from flink_siddhi import shuffle
+    plan = workload.PATTERN_PLAN
+    senders = [fs.SiddhiAppRuntime(plan, ts_order=1) for _ in range(world)]
+    owners = [fs.SiddhiAppRuntime(plan, ts_order=1, key_stride=world, key_offset=r, chunk_events=8192)
+              for r in range(world)]
+    for o in owners:
+        o.add_callback("O")
+    allw = []
+    spilled_steps = 0
+    for s in range(steps):
+        sent, spills = [], []
+        for src in range(world):
+            g = s * world + src
+            w = workload.generate(g * n_per, n_per, keys, rate=1)
+            if skew_step is not None and s >= skew_step:
+                w["k"] = np.where(w["k"] % 5 != 0, (w["k"] // world) * world, w["k"]).astype(np.int32)
+            allw.append(w)
+            d = _dev(w)
+            words = senders[src].record_words()
+            sbuf = torch.zeros((n_per, words), dtype=torch.int64, device="cuda")
+            scnt = torch.zeros(world, dtype=torch.int64, device="cuda")
+            segs = senders[src].route_padded("A", d["ts"], [d["k"], d["ts"], d["id"], d["price"]],
+                                             world, seq0=g * n_per, seg_cap=seg_cap, streams=d["stream"],
+                                             spill=(sbuf, scnt))
+            sent.append(segs)
+            spills.append((sbuf, scnt))
+        torch.cuda.synchronize()
+        S = 1 + seg_cap
+        scounts = [[int(x) for x in sc.cpu().tolist()] for _, sc in spills]
+        any_spill = sum(map(sum, scounts)) > 0
+        spilled_steps += any_spill
+        for r in range(world):
+            recv = torch.cat([sent[src][r * S:(r + 1) * S] for src in range(world)], dim=0)
+            if not any_spill:
+                owners[r].send_padded(recv, world, seg_cap, n_per)
+                continue
+            # the exact spill exchange, simulated: source src's spill for
+            # owner r is its r-th owner group
+            parts, src_counts = [], []
+            for src in range(world):
+                off = sum(scounts[src][:r])
+                c = scounts[src][r]
+                parts.append(spills[src][0][off:off + c])
+                src_counts.append(c)
+            merged = shuffle.merge_padded(recv, world, seg_cap, torch.cat(parts, dim=0), src_counts)
+            owners[r].send_records(merged, int(merged.shape[0]), n_per)
+    return senders, owners, allw, spilled_steps
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_padded_spill_survives_a_key_skew_shift(world):
+    # VERDICT r04 item 6: a key-distribution shift that overflows seg_cap
+    # mid-stream must not drop records or fail the job: every row vs the
+    # oracle over the whole stream
+    n_per, keys, steps = 12000, 600, 4
+    from flink_siddhi import shuffle
+    cap = shuffle.padded_capacity(n_per // 3, world, slack=0.25, floor=64)
+    senders, owners, allw, spilled = _spill_round(world, n_per, keys, cap, steps, skew_step=2)
+    assert spilled >= 2, "the skewed steps must overflow seg_cap"
+    got = []
+    for o in owners:
+        o.flush()   # no CEP_E_CAPACITY: nothing was dropped
+        got += engine_rows(o.collect("O"))
+    got.sort(key=lambda t: t[1])
+    w = {c: np.concatenate([x[c] for x in allw]) for c in allw[0]}
+    want = oracle_run(workload.PATTERN_PLAN, workload_events(w)).get("O", [])
+    assert len(want) > 100
+    assert_same_rows(got, want, "padded spill world=%d" % world)
+    for rt in owners + senders:
+        rt.shutdown()
