@@ -231,13 +231,15 @@ def host_cores():
     return use, n, quota
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (scripts/gpu_pmc.sh -> scripts/pmc_summary.py -> profiles/rNN_pmc.json;
-    FETCH_SIZE doubled per the gfx950 caveat), measured in separate
-    rocprofv3 --pmc passes of this same bench command; null if absent."""
+    of this workload (scripts/gpu_pmc.sh -> scripts/pmc_summary.py ->
+    profiles/rNN_pmc_<workload>.json; FETCH_SIZE doubled per the gfx950
+    caveat), measured in separate rocprofv3 --pmc passes of the same bench
+    command; null if no summary of this workload exists (a Zipf run is never
+    credited with the uniform run's counters)."""
     import glob
-    files = sorted(glob.glob(str(ROOT / "profiles" / "*pmc*.json")))
+    files = sorted(glob.glob(str(ROOT / "profiles" / ("r*_pmc_%s.json" % workload))))
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -580,7 +582,10 @@ def main():
             # calibrate the segment capacity on the first warm-up step
             # (two-phase: host counts), then every later step is padded
             recs, counts = route(blist[0], 0)
-            seg_cap[0] = shuffle.calibrated_capacity(counts)
+            # 3 % over the largest owner: records past it spill (PaddedShuffle),
+            # so the slack only sizes the common case, and every padding
+            # record is bytes on xGMI and a null record for the owner
+            seg_cap[0] = shuffle.calibrated_capacity(counts, slack=0.03)
             recv, m, _ = shuffle.exchange(recs, counts, out=bufs.get(("recv", 0)))
             bufs[("recv", 0)] = recv
             send_fn(recv, m, n, signal=False)
@@ -684,6 +689,10 @@ def main():
             design["k_mqwalk"] += kern["k_mqwalk"]["launches"] * keys_local * st_words * 8 * 2
     else:
         design = {"k_filter": ev_total * (FILTER_IN_BYTES + FILTER_OUT_BYTES * m_per_event)}
+    # PMC summaries are per workload (scripts/gpu_pmc.sh runs of the default
+    # config-3 / filter / config-5 commands)
+    pmc_tag = ("config3" if args.keys_dist == "uniform" else "zipf") if pattern else \
+        ("config5" if config5 else "filter")
     per_kernel = {}
     for kname, b in design.items():
         if kname not in kern:
@@ -692,7 +701,7 @@ def main():
         ach = per_launch / (kern[kname]["avg_us"] * 1e-6) / 1e9
         per_kernel[kname] = {"design_bytes_per_launch": round(per_launch), "avg_launch_us": kern[kname]["avg_us"],
                              "design_achieved": round(ach, 1), "design_frac": round(ach / HBM_PEAK_GBS, 4),
-                             "traffic": pmc_traffic(kname) if world == 1 else None}
+                             "traffic": pmc_traffic(kname, pmc_tag) if world == 1 else None}
     roofline = None
     if kern:   # CEP_PROFILE=0 (no per-kernel timer events): no kernel roofline
         # the dominant kernel (largest share of the step's kernel time),
@@ -701,7 +710,7 @@ def main():
         ev_launch = ev_total / kern[dom]["launches"]
         alg_launch = alg_per_event * ev_launch
         ach = alg_launch / (kern[dom]["avg_us"] * 1e-6) / 1e9
-        tr = pmc_traffic(dom) if world == 1 else None
+        tr = pmc_traffic(dom, pmc_tag) if world == 1 else None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": tr["bytes_per_launch"] if tr else None,

@@ -15,7 +15,7 @@ import sys
 
 def short(name):
     for k in ("k_cfpart", "k_cfwalk", "k_mqpart", "k_mqwalk", "k_partition", "k_walk", "k_filter", "k_generate",
-              "k_route"):
+              "k_cfroute", "k_route_gather", "k_route_pad", "k_route_scan", "k_route"):
         if k in name:
             return k
     return None
