@@ -7,8 +7,10 @@ K = 2^20 partition keys, N = 2^28 events per step, R = 400 events/ms.
 A step = one pass of the hot path (predicate + key-bucket partition + per-key
 NFA walk + match emission) over one batch of N events already resident in
 HBM; the per-key pattern state carries from step to step (each step is the
-next N events of one stream).  With --gpus N > 1 (torchrun), each rank owns
-the keys k % N == rank and processes N events per step (weak scaling).
+next N events of one stream).  With --gpus N > 1 each rank owns the keys
+k % N == rank and processes N events per step (weak scaling); without
+WORLD_SIZE in the environment bench.py starts the N rank processes itself
+(launch_ranks), under torchrun it uses the ranks it is given.
 
 `--workload filter` runs configs[1] (config 2): `inputStream[price > 0.5 and
 id % 7 == 0] select *` over 10^8 events.
