@@ -37,6 +37,15 @@ namespace cep {
 namespace {
 
 constexpr uint16_t kNoB = 0xffff;
+// Order-tolerant records (TOL builds, cep_options.ts_order 0): a B-stream row
+// that fails g is kept with this role — it completes nothing but expires the
+// partials it is more than W away from (App. A.3, on every event of the
+// waiting stream) — and record ts are stored as ts - chunk base + 2^31.
+constexpr uint32_t kRolePB = 4;
+constexpr int64_t kTolBias = 1ll << 31;
+// skr bit 15 (TOL walk): the A at this sorted position survives every B-stream
+// row up to its next g-passing B (or to the end of its run)
+constexpr uint32_t kSkrAlive = 0x8000u;
 constexpr int kCfStageBytes = (kCfTile / 8192 * 20 + 36) * 1024;    // a tile keeps ~1/3 of its rows at config 3
 
 // Diagnostics (CEP_STAMPS=1): s_memtime at phase i of block b.
@@ -101,7 +110,8 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 #ifndef CF_PART_MINW   // waves per SIMD the register budget is set for
 #define CF_PART_MINW (kCfPartThreads == 512 ? 4 : 1)
 #endif
-template <int NW, bool FR, int NP = kPref>   // FR: rows are received shuffle records; NP prefetched columns
+// FR: rows are received shuffle records; NP prefetched columns; TOL: order-tolerant records
+template <int NW, bool FR, int NP = kPref, bool TOL = false>
 __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
   constexpr int kStageRecs = kCfStageBytes / (8 * RW);
@@ -131,7 +141,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
   uint32_t valid = 0;
 #pragma unroll
   for (int e = 0; e < E; ++e) valid |= (r0 + 64 * e < a.rows.n ? 1u : 0u) << e;
-  uint32_t role_a = 0, role_b = 0;
+  uint32_t role_a = 0, role_b = 0, role_pb = 0;
   uint64_t tsv[E];
   uint64_t pv[NP][E];
 #pragma unroll
@@ -184,7 +194,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
         is_b |= ((int)sb[e] == p.b_stream ? 1u : 0u) << e;
       }
     }
-    if (p.within >= 0) {
+    if (p.within >= 0 && !TOL) {
       // event-time order check (`within` pruning relies on it): row r - 1 is
       // held by the previous lane (same e), lane 63 (e - 1), or loaded
       const int64_t before = row0 > 0 ? a.rows.ts[row0 - 1] : batch_prev_ts(a.rows);
@@ -201,6 +211,7 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
     const uint32_t all = (1u << E) - 1u;
     if (is_a) role_a = is_a & (p.f_prog < 0 ? all : eval_terms_regs<E, NP>(p.f_terms, a.pref.f_slot, a.rows.cols, pv));
     if (is_b) role_b = is_b & (p.g_raw_prog < 0 ? all : eval_terms_regs<E, NP>(p.g_terms, a.pref.g_slot, a.rows.cols, pv));
+    if (TOL) role_pb = is_b & ~role_b;
     // key (the host puts the key column in slot 0) and carried words (A
     // rows: the A's columns, else the B's) picked now, so pv dies here
     if (NW > 0) pick_carried<E, NP>(pv, a.cf.a_slot[0], a.cf.b_slot[0], role_a, fc0);
@@ -213,14 +224,15 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
   lds_barrier();   // hist zeroed
   CF_STAMP(1);
 
-  // bits 0-12 rank in tile, 13-24 bucket, 25-26 role (never all ones)
+  // bits 0-12 rank in tile, 13-24 bucket, 25-27 role (never all ones)
   uint32_t packed[E];
   uint32_t lkey[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     packed[e] = 0xffffffffu;
     lkey[e] = 0;
-    const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B;
+    const uint32_t role = ((role_a >> e) & 1u) * ROLE_A | ((role_b >> e) & 1u) * ROLE_B |
+                          (TOL ? ((role_pb >> e) & 1u) * kRolePB : 0u);
     if (!role) continue;
     int64_t key;
     key = (int64_t)fkey[e];
@@ -278,9 +290,13 @@ __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartA
     const uint32_t b = (packed[e] >> 13) & 0xfffu;
     const uint32_t role = packed[e] >> 25;
     const uint32_t slot = hist[b] + (packed[e] & 0x1fffu);
-    const int64_t dts = (int64_t)tsv[e] - ts_base;
-    if (dts < 0) report_descent(a.rows, a.err);
-    else if (dts > 0xffffffffll) set_err(a.err, ERR_TS_SPAN);
+    const int64_t dts = (int64_t)tsv[e] - ts_base + (TOL ? kTolBias : 0);
+    if (dts < 0) {
+      if (TOL) set_err(a.err, ERR_TS_SPAN);
+      else report_descent(a.rows, a.err);
+    } else if (dts > 0xffffffffll) {
+      set_err(a.err, ERR_TS_SPAN);
+    }
     const uint64_t w0 = (uint64_t)(uint32_t)dts | ((uint64_t)(wave * 64 * E + 64 * e + lane) << 32) |
                         ((uint64_t)role << 45) | ((uint64_t)lkey[e] << 48);
     const uint64_t c0 = fc0[e], c1 = fc1[e];
@@ -570,7 +586,9 @@ __device__ __forceinline__ void cf_emit(const CfWalkArgs& a, unsigned long long 
 
 }  // namespace
 
-template <int NW, bool KR, int NC>   // NC: captured words per pending slot (slot_words - 2)
+// NC: captured words per pending slot (slot_words - 2); TOL: order-tolerant
+// records (ts in any order, App. A.3's |ts - ts(s1)| > W on every B-stream row)
+template <int NW, bool KR, int NC, bool TOL = false>
 __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   // 2 workgroups per CU
   constexpr int NT = kCfWalkThreads, RW = 1 + NW, WIN = cf_window<NW>();
   constexpr int TPT = kCfMaxTiles / NT;   // tiles per thread
@@ -689,7 +707,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     return (m0 & ((t0r & w0) | (a0c0 & w2) | (a0c1 & w3))) |
            (m1 & ((t1r & w0) | (a1c0 & w2) | (a1c1 & w3)));
   };
-  const int64_t ts_base = a.chunk_base[0];
+  const int64_t ts_base = a.chunk_base[0] - (TOL ? kTolBias : 0);   // record ts = ts_base + sts
   const int64_t seq_base = a.chunk_base[1];
   int kbuf = 0;   // this window's key-run buffer
   for (int k = tid; k <= kpb; k += NT) L.kstart[0][k] = 0;
@@ -1031,12 +1049,46 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
     uint32_t r0 = 0, r1 = 0;
     int cfirst = 0, cm = 0;
     uint64_t e00 = 0, e01 = 0, e10 = 0, e11 = 0;
+    // TOL: ts range [tmn, tmx] (sts units) of the B-stream rows from the run
+    // start to its first g-passing B inclusive (the whole run without one)
+    uint32_t tmn = 0xffffffffu, tmx = 0u;
+    bool thave = false;
+    auto tol_alive = [&](int64_t pts) {   // a partial started at pts survives that range
+      return !thave || W < 0 ||
+             (pts - (ts_base + (int64_t)tmn) <= W && (ts_base + (int64_t)tmx) - pts <= W);
+    };
     if (klane) {
       r0 = L.kstart[kbuf][tid];
       r1 = L.kstart[kbuf][tid + 1];
       kcnt += r1 - r0;
       const uint16_t fb = L.kfb[tid];
-      if (r1 > r0 && fb != kNoB && n > 0) {
+      if (TOL && r1 > r0) {
+        // right to left over the key's run: each A learns whether every
+        // B-stream row after it up to its next g-passing B (inclusive) is
+        // within W of it (skr bit 15); the range restarts at each such B
+        for (uint32_t q = r1; q-- > r0;) {
+          const uint32_t kr = L.skr[q];
+          const uint32_t role = (kr >> 12) & 7u;
+          const uint32_t t = L.sts[q];
+          if (role & ROLE_A) {
+            const bool ok = !thave || W < 0 ||
+                            ((int64_t)t - (int64_t)tmn <= W && (int64_t)tmx - (int64_t)t <= W);
+            L.skr[q] = (uint16_t)((kr & 0x7fffu) | (ok ? kSkrAlive : 0u));
+          }
+          if (role & ROLE_B) {
+            tmn = tmx = t;
+            thave = true;
+          } else if (role & kRolePB) {
+            tmn = t < tmn ? t : tmn;
+            tmx = t > tmx ? t : tmx;
+            thave = true;
+          }
+        }
+        // carried partials completed by the first g-passing B: every one
+        // that survives the rows before it (not a prefix when ts go back)
+        if (fb != kNoB)
+          for (int j = 0; j < n; ++j) cm += tol_alive((int64_t)slot_word(j, 0)) ? 1 : 0;
+      } else if (!TOL && r1 > r0 && fb != kNoB && n > 0) {
         const int64_t tb = ts_base + (int64_t)L.sts[fb];
         cfirst = n;
         for (int j = 0; j < n; ++j) {
@@ -1051,11 +1103,11 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       L.cm[tid] = (uint8_t)cm;
       // captures of the first two completed carried partials (registers
       // unless the partial sits in slot >= 2)
-      if (cm > 0) {
+      if (!TOL && cm > 0) {
         e00 = c1 ? slot_word(cfirst, 2) : 0ull;
         e01 = c2 ? slot_word(cfirst, 3) : 0ull;
       }
-      if (cm > 1) {
+      if (!TOL && cm > 1) {
         e10 = c1 ? slot_word(cfirst + 1, 2) : 0ull;
         e11 = c2 ? slot_word(cfirst + 1, 3) : 0ull;
       }
@@ -1099,8 +1151,12 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
           const uint32_t k = kr & 0xfffu;
           const uint32_t nb = nbv[i];
           if (((kr >> 12) & ROLE_A) && nb != kNoB) {
-            const int64_t d = (int64_t)L.sts[nb] - (int64_t)stv[i];
-            val = (W < 0 || (d < 0 ? -d : d) <= W) ? (1u << 20) | 1u : 0u;
+            if (TOL) {
+              val = (kr & kSkrAlive) ? (1u << 20) | 1u : 0u;
+            } else {
+              const int64_t d = (int64_t)L.sts[nb] - (int64_t)stv[i];
+              val = (W < 0 || (d < 0 ? -d : d) <= W) ? (1u << 20) | 1u : 0u;
+            }
           }
           if (q == L.kstart[kbuf][k]) val += L.cm[k];
         }
@@ -1154,14 +1210,25 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         CF_COUNT(0, cm);
         const int64_t bts = ts_base + (int64_t)L.sts[fb];
         const uint64_t b0 = NW > 0 ? L.scap[0][fb] : 0ull, b1 = NW > 1 ? L.scap[NW > 1 ? 1 : 0][fb] : 0ull;
-        for (int j = 0; j < cm; ++j) {
-          const int js = cfirst + j;
-          const uint64_t x0 = j == 0 ? e00 : (j == 1 ? e10 : (c1 ? slot_word(js, 2) : 0ull));
-          const uint64_t x1 = j == 0 ? e01 : (j == 1 ? e11 : (c2 ? slot_word(js, 3) : 0ull));
-          cf_emit<KR>(a, base + L.v[r0] + j, kv, x0, x1, b0, b1, bts, seq_base + (int64_t)L.sseq[fb]);
+        if (TOL) {   // the carried partials that survived to the first B, in slot order
+          int o = 0;
+          for (int j = 0; j < n && o < cm; ++j) {
+            if (!tol_alive((int64_t)slot_word(j, 0))) continue;
+            cf_emit<KR>(a, base + L.v[r0] + o, kv, c1 ? slot_word(j, 2) : 0ull, c2 ? slot_word(j, 3) : 0ull,
+                        b0, b1, bts, seq_base + (int64_t)L.sseq[fb]);
+            ++o;
+          }
+        } else {
+          for (int j = 0; j < cm; ++j) {
+            const int js = cfirst + j;
+            const uint64_t x0 = j == 0 ? e00 : (j == 1 ? e10 : (c1 ? slot_word(js, 2) : 0ull));
+            const uint64_t x1 = j == 0 ? e01 : (j == 1 ? e11 : (c2 ? slot_word(js, 3) : 0ull));
+            cf_emit<KR>(a, base + L.v[r0] + j, kv, x0, x1, b0, b1, bts, seq_base + (int64_t)L.sseq[fb]);
+          }
         }
       }
-      const bool prune = W >= 0 && L.khasa[tid];
+      // (TOL: no pruning at A arrivals — a later row may carry an older ts)
+      const bool prune = !TOL && W >= 0 && L.khasa[tid];
       const int64_t last_a_ts = ts_base + (int64_t)L.klast[tid];
       // new pending list, built in place: (no B in the run) the carried
       // partials minus the pruned prefix, then the starts after the last B
@@ -1214,6 +1281,20 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       };
       if (lb == kNoB && (a.ablate & 1)) {
         nn = 0;
+      } else if (TOL && lb == kNoB) {
+        // no g-passing B: the carried partials that survive the run's B-stream rows
+        bool all = true;
+        for (int j = 0; j < n && all; ++j) all = tol_alive((int64_t)slot_word(j, 0));
+        if (all && cap <= S) {
+          nn = n;   // unchanged, in place
+        } else {
+          for (int j = 0; j < n; ++j) {
+            const uint64_t ts = slot_word(j, 0);
+            if (!tol_alive((int64_t)ts)) continue;
+            const uint64_t x0 = c1 ? slot_word(j, 2) : 0ull, x1 = c2 ? slot_word(j, 3) : 0ull;
+            put_slot(ts, x0, x1);
+          }
+        }
       } else if (lb == kNoB) {
         int drop = 0;
         while (drop < n && prune && last_a_ts - (int64_t)slot_word(drop, 0) > W) ++drop;
@@ -1232,6 +1313,7 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       // starts a partial after completing others)
       for (uint32_t q = (lb == kNoB ? r0 : (uint32_t)lb); q < r1 && !(a.ablate & 2); ++q) {
         if (!((L.skr[q] >> 12) & ROLE_A)) continue;
+        if (TOL && !(L.skr[q] & kSkrAlive)) continue;   // expired before the run ended
         const int64_t ats = ts_base + (int64_t)L.sts[q];
         if (prune && last_a_ts - ats > W) continue;
         if (nn >= cap) {   // only after the pool ran out (ERR_POOL is set)
@@ -1265,8 +1347,12 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
       const uint32_t kr = L.skr[q];
       const uint16_t nb = L.nextb[q];
       if (!((kr >> 12) & ROLE_A) || nb == kNoB) continue;
-      const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
-      if (W >= 0 && (d < 0 ? -d : d) > W) continue;
+      if (TOL) {
+        if (!(kr & kSkrAlive)) continue;
+      } else {
+        const int64_t d = (int64_t)L.sts[nb] - (int64_t)L.sts[q];
+        if (W >= 0 && (d < 0 ? -d : d) > W) continue;
+      }
       const uint32_t k = kr & 0xfffu;
       const uint32_t extra = q == L.kstart[kbuf][k] ? L.cm[k] : 0u;
       const int64_t ats = ts_base + (int64_t)L.sts[q];
@@ -1370,6 +1456,20 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
   }
   // the local-rows build holds only the prefetched columns the plan reads
   const int np = a.pref.n <= 2 ? 2 : a.pref.n;
+  if (a.pat.tolerant) {   // order-tolerant records (cep_options.ts_order 0)
+    switch (a.cf.nw * 8 + np) {
+      case 0 * 8 + 2: hipLaunchKernelGGL((k_cfpart<0, false, 2, true>), g, b, dyn, s, a); break;
+      case 0 * 8 + 3: hipLaunchKernelGGL((k_cfpart<0, false, 3, true>), g, b, dyn, s, a); break;
+      case 0 * 8 + 4: hipLaunchKernelGGL((k_cfpart<0, false, 4, true>), g, b, dyn, s, a); break;
+      case 1 * 8 + 2: hipLaunchKernelGGL((k_cfpart<1, false, 2, true>), g, b, dyn, s, a); break;
+      case 1 * 8 + 3: hipLaunchKernelGGL((k_cfpart<1, false, 3, true>), g, b, dyn, s, a); break;
+      case 1 * 8 + 4: hipLaunchKernelGGL((k_cfpart<1, false, 4, true>), g, b, dyn, s, a); break;
+      case 2 * 8 + 2: hipLaunchKernelGGL((k_cfpart<2, false, 2, true>), g, b, dyn, s, a); break;
+      case 2 * 8 + 3: hipLaunchKernelGGL((k_cfpart<2, false, 3, true>), g, b, dyn, s, a); break;
+      default: hipLaunchKernelGGL((k_cfpart<2, false, 4, true>), g, b, dyn, s, a); break;
+    }
+    return;
+  }
   switch (a.cf.nw * 8 + np) {
     case 0 * 8 + 2: hipLaunchKernelGGL((k_cfpart<0, false, 2>), g, b, dyn, s, a); break;
     case 0 * 8 + 3: hipLaunchKernelGGL((k_cfpart<0, false, 3>), g, b, dyn, s, a); break;
@@ -1383,18 +1483,26 @@ void launch_cf_partition(const CfPartArgs& a, int64_t ntiles, hipStream_t s) {
   }
 }
 
-template <int NW, bool KR>
+template <int NW, bool KR, bool TOL = false>
 static void launch_cf_walk_nc(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
   const dim3 g((unsigned)nbuckets), b(kCfWalkThreads);
   switch (a.pat.slot_words - 2) {
-    case 0: hipLaunchKernelGGL((k_cfwalk<NW, KR, 0>), g, b, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((k_cfwalk<NW, KR, 1>), g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL((k_cfwalk<NW, KR, 2>), g, b, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((k_cfwalk<NW, KR, 0, TOL>), g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_cfwalk<NW, KR, 1, TOL>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_cfwalk<NW, KR, 2, TOL>), g, b, 0, s, a); break;
   }
 }
 
 void launch_cf_walk(const CfWalkArgs& a, int nbuckets, hipStream_t s) {
   const bool kr = a.key_rev != nullptr;
+  if (a.pat.tolerant) {   // order-tolerant records (dense keys only: the engine refuses sparse + tolerant)
+    switch (a.cf.nw) {
+      case 0: launch_cf_walk_nc<0, false, true>(a, nbuckets, s); break;
+      case 1: launch_cf_walk_nc<1, false, true>(a, nbuckets, s); break;
+      default: launch_cf_walk_nc<2, false, true>(a, nbuckets, s); break;
+    }
+    return;
+  }
   switch (a.cf.nw) {
     case 0: kr ? launch_cf_walk_nc<0, true>(a, nbuckets, s) : launch_cf_walk_nc<0, false>(a, nbuckets, s); break;
     case 1: kr ? launch_cf_walk_nc<1, true>(a, nbuckets, s) : launch_cf_walk_nc<1, false>(a, nbuckets, s); break;

@@ -125,6 +125,7 @@ struct PatternRT {
   bool used[2] = {false, false};
   int cur = 0;                 // arena of the next chunk
   int64_t chunk = 0;
+  int64_t chunk_tol = 0;       // chunk of the order-tolerant form (walked by the VM build: up to 16 Mi rows)
   int64_t extra_bound = 0;   // pending partials that may still complete
   bool part_vm = true;       // partition pass needs the interpreter
   bool walk_vm = true;       // walk needs the interpreter (g on s1, computed select items)
@@ -1069,9 +1070,20 @@ int create_runtime(cep_app* a) {
                                          kPartThreads * kPartItems);
     chunk = (chunk / (kPartThreads * kPartItems)) * (kPartThreads * kPartItems);
     rt.chunk = chunk;
-    const int64_t ntiles = chunk / (kPartThreads * kPartItems);
+    // the order-tolerant form of a `within` pattern (ts_order 0, released
+    // late rows) runs on the VM walk, whose segment tables hold 4x the tiles:
+    // its chunks may be that long, so per-key state is loaded and committed
+    // a quarter as often
+    int64_t chunk_tol = chunk;
+    if (!walk_vm && q.within >= 0) {
+      chunk_tol = std::max<int64_t>(a->opt.chunk_events, kPartThreads * kPartItems);
+      chunk_tol = std::min<int64_t>(chunk_tol, (int64_t)kWalkMaxTiles * kPartThreads * kPartItems);
+      chunk_tol = (chunk_tol / (kPartThreads * kPartItems)) * (kPartThreads * kPartItems);
+    }
+    rt.chunk_tol = chunk_tol;
+    const int64_t ntiles = std::max(chunk, chunk_tol) / (kPartThreads * kPartItems);
     for (int b = 0; b < 2; ++b) {
-      if (!dev_ensure(&rt.recs[b], (size_t)chunk * p.rec_words * 8 + 16, a->stream, false) ||
+      if (!dev_ensure(&rt.recs[b], (size_t)std::max(chunk, chunk_tol) * p.rec_words * 8 + 16, a->stream, false) ||
           !dev_ensure(&rt.tile_off[b], (size_t)ntiles * ((1 << lg) + 1) * 2, a->stream, false))
         return fail(a, CEP_E_DEVICE, "out of device memory (record arena)");
       if (hipEventCreateWithFlags(&rt.part_done[b], hipEventDisableTiming) != hipSuccess ||
@@ -1359,10 +1371,13 @@ bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf, bool from_re
 
 // Closed-form fast path: k_cfpart(c) then k_cfwalk(c) per chunk (double-
 // buffered arenas; CEP_OVERLAP=1 runs the partitions on the side stream).
+// tol: the order-tolerant closed form (ts in any order: g-failing B rows kept
+// as expiry-only records, no pruning at A arrivals, no hot-key diversion).
 int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
                    const RowsArgs& rows_all, const CfPlan& cf,
-                   const uint64_t* in_recs = nullptr, int in_rec_words = 0) {
+                   const uint64_t* in_recs = nullptr, int in_rec_words = 0, bool tol = false) {
   const int P = 1 << rt.pa.buckets_log2;
+  const bool hot_ok = rt.hot && !tol;
   // Both passes on the main stream by default: k_cfpart and k_cfwalk cannot
   // share a CU (each fills its register file), so the side stream only
   // time-slices them (measured: no throughput gain, inflated kernel times).
@@ -1385,7 +1400,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
   for (int64_t r0 = 0, step = 0; r0 < rows_all.n; r0 += step) {
     const int b = rt.cur;
     rt.cur ^= 1;
-    const bool probe = rt.hot && !rt.hot_on && !rt.hot_probed;
+    const bool probe = hot_ok && !rt.hot_on && !rt.hot_probed;
     step = std::min<int64_t>(probe ? std::min<int64_t>(kHotProbeRows, rt.cf_chunk) : rt.cf_chunk, rows_all.n - r0);
     RowsArgs rows = rows_all;
     rows.row0 = rows_all.row0 + r0;
@@ -1402,6 +1417,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       if (rows.cols.p[rt.pref.col[i]] == (const void*)rows.ts && rows.cols.t[rt.pref.col[i]] == T_LONG)
         pa.ts_slot = i;
     pa.pat = rt.pa;
+    pa.pat.tolerant = tol ? 1 : 0;
     pa.cf = cf;
     pa.chunk_base = (int64_t*)rt.chunk_base[b].p;
     pa.recs = (uint64_t*)rt.cf_recs[b].p;
@@ -1411,7 +1427,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     if (a->stamps.p) pa.stamps = (uint64_t*)a->stamps.p + 4096 * 16;
     // hot keys: diversion starts once the device reported a slot in use (the
     // pinned word is refreshed asynchronously after every walk)
-    const bool hot = rt.hot;
+    const bool hot = hot_ok;
     if (hot && !rt.hot_on && *(volatile uint32_t*)rt.hot_active_host.p > 0) {
       const int rw = 1 + cf.nw;
       const int64_t cc = rt.cf_chunk, ntmax = cc / kCfTile;
@@ -1446,7 +1462,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       hipStreamWaitEvent(a->stream, rt.part_done[b], 0);
     }
     CfWalkArgs wa{};
-    wa.pat = rt.pa;
+    wa.pat = pa.pat;
     wa.cf = cf;
     wa.recs = pa.recs;
     wa.tile_off = pa.tile_off;
@@ -1541,7 +1557,11 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     if (hot) {
       if (divert && !hot_serial) hipStreamWaitEvent(a->stream, rt.hot_join, 0);
       launch_hot_update(ha, divert ? 1 : 0, a->stream);
-      hipMemcpyAsync(rt.hot_active_host.p, rt.hot_active.p, 4, hipMemcpyDeviceToHost, a->stream);
+      // slots in use, for the next batch's diversion check and cep_stats:
+      // once per batch (and after the probe), not per chunk — each copy is
+      // a blit on the engine stream between two walks
+      if (probe || r0 + step >= rows_all.n)
+        hipMemcpyAsync(rt.hot_active_host.p, rt.hot_active.p, 4, hipMemcpyDeviceToHost, a->stream);
       if (probe) {   // the probe's verdict decides the next chunk's diversion
         hipStreamSynchronize(a->stream);
         rt.hot_probed = true;
@@ -1659,6 +1679,14 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_in,
     if (cf_plan(rt, rows_all, &cf, in_recs != nullptr))
       return run_pattern_cf(a, rt, q, o, rows_all, cf, in_recs, in_rec_words);
   }
+  // ts in any order on the closed form (k_cfpart / k_cfwalk TOL builds);
+  // CEP_TOL_GENERAL=1 keeps the N-state walk (nfa_pair) for these runs
+  static const bool tol_general = std::getenv("CEP_TOL_GENERAL") != nullptr;
+  if (rt.cf && tolerant && !tol_general && !in_recs && !rows_all.seq && pref_aligned(rt.pref, rows_all)) {
+    CfPlan cf;
+    if (cf_plan(rt, rows_all, &cf, false))
+      return run_pattern_cf(a, rt, q, o, rows_all, cf, nullptr, 0, true);
+  }
   const int P = 1 << rt.pa.buckets_log2;
   // the side stream starts after everything already queued on the main stream
   // (host-batch staging copies, earlier queries)
@@ -1667,12 +1695,13 @@ int run_pattern(cep_app* a, PatternRT& rt, const RowsArgs& rows_in,
   // CEP_NO_OVERLAP=1 (diagnostics): both passes on the main stream
   static const bool no_overlap = std::getenv("CEP_NO_OVERLAP") != nullptr;
   hipStream_t side = no_overlap ? a->stream : a->side;
-  for (int64_t r0 = 0; r0 < rows_all.n; r0 += rt.chunk) {
+  const int64_t cstep = tolerant ? rt.chunk_tol : rt.chunk;
+  for (int64_t r0 = 0; r0 < rows_all.n; r0 += cstep) {
     const int b = rt.cur;
     rt.cur ^= 1;
     RowsArgs rows = rows_all;
     rows.row0 = rows_all.row0 + r0;
-    rows.n = std::min<int64_t>(rt.chunk, rows_all.n - r0);
+    rows.n = std::min<int64_t>(cstep, rows_all.n - r0);
     if (r0 > 0) rows.prev_ts = INT64_MIN;   // checked inside the kernel via ts[row-1]
     const int64_t ntiles = (rows.n + kPartThreads * kPartItems - 1) / (kPartThreads * kPartItems);
     PartArgs pa{};

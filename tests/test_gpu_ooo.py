@@ -8,11 +8,12 @@ processed (core/.../operator/AbstractSiddhiOperator.java:222-231, 238-245).
 Processing time (:218-219) and direct callers can also hand Siddhi a ts
 below one it has seen.  Siddhi then prunes a partial when |ts(event) -
 ts(s1)| > W on every event of the stream the partial waits on (SURVEY App.
-A.3, the rule both oracles implement).  The engine runs its event-time fast
-paths speculatively, notices a descent on the device and re-runs the batch
-from the first affected chunk on the order-tolerant path
-(cep_options.ts_order = 0, the default); late_policy = 2 (default) delivers
-late rows as the reference's drain does.
+A.3, the rule both oracles implement).  With cep_options.ts_order = 0 (the
+default) the engine runs every `within` pattern on its order-tolerant form
+(the closed form's TOL build for `every A -> B`, tests/test_gpu_ooo_cf.py; the
+N-state walk otherwise); ts_order = 1 keeps the event-time fast paths and
+reports a descent.  late_policy = 2 (default) delivers late rows as the
+reference's drain does.
 
 Every case is bit-exact against oracle/siddhi_oracle.py fed exactly the
 sequence the reference would hand Siddhi.
