@@ -151,7 +151,7 @@ struct PatternRT {
   uint32_t hot_thresh = 0;     // records per key per launch that make a key hot
   int hot_blocks = 0;
   DevBuf hot_id, hot_key, hot_m, hot_gbase, hoff, cand, ncand, harr, hrow, hnb, bsum, bcnt, boff, hcm, hobase,
-      hot_active;
+      hot_active, htmn, htmx, hflag, btol;   // (the last four: order-tolerant runs)
   HostBuf hot_active_host;     // pinned: slots in use (read without a sync)
   hipEvent_t hot_fork = nullptr, hot_join = nullptr;   // hot kernels on the side stream, beside the walk
   // a pattern whose result depends on event-time order (`within`, not a
@@ -1372,12 +1372,13 @@ bool cf_plan(const PatternRT& rt, const RowsArgs& rows, CfPlan* cf, bool from_re
 // Closed-form fast path: k_cfpart(c) then k_cfwalk(c) per chunk (double-
 // buffered arenas; CEP_OVERLAP=1 runs the partitions on the side stream).
 // tol: the order-tolerant closed form (ts in any order: g-failing B rows kept
-// as expiry-only records, no pruning at A arrivals, no hot-key diversion).
+// as expiry-only records, no pruning at A arrivals; hot keys through the
+// hot kernels' order-tolerant scans).
 int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
                    const RowsArgs& rows_all, const CfPlan& cf,
                    const uint64_t* in_recs = nullptr, int in_rec_words = 0, bool tol = false) {
   const int P = 1 << rt.pa.buckets_log2;
-  const bool hot_ok = rt.hot && !tol;
+  const bool hot_ok = rt.hot;
   // Both passes on the main stream by default: k_cfpart and k_cfwalk cannot
   // share a CU (each fills its register file), so the side stream only
   // time-slices them (measured: no throughput gain, inflated kernel times).
@@ -1441,7 +1442,11 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
                       dev_ensure(&rt.bcnt, (size_t)rt.hot_blocks * 4, a->stream, false) &&
                       dev_ensure(&rt.boff, (size_t)rt.hot_blocks * 4, a->stream, false) &&
                       dev_ensure(&rt.hcm, kCfHotMax * 3 * 4, a->stream, false) &&
-                      dev_ensure(&rt.hobase, 64, a->stream, false);
+                      dev_ensure(&rt.hobase, 64, a->stream, false) &&
+                      dev_ensure(&rt.htmn, (size_t)cc * 4, a->stream, false) &&
+                      dev_ensure(&rt.htmx, (size_t)cc * 4, a->stream, false) &&
+                      dev_ensure(&rt.hflag, (size_t)cc, a->stream, false) &&
+                      dev_ensure(&rt.btol, (size_t)rt.hot_blocks * 12, a->stream, false);
       if (!ok) return fail(a, CEP_E_DEVICE, "out of device memory (hot-key arenas)");
       rt.hot_on = true;
     }
@@ -1482,7 +1487,7 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
     wa.err = pa.err;
     HotArgs ha{};
     if (hot) {
-      ha.pat = rt.pa;
+      ha.pat = pa.pat;   // (tolerant flag included)
       ha.cf = cf;
       ha.recs = pa.recs;
       ha.tile_off = pa.tile_off;
@@ -1505,6 +1510,10 @@ int run_pattern_cf(cep_app* a, PatternRT& rt, const Query& q, OutStream& o,
       ha.boff = (uint32_t*)rt.boff.p;
       ha.hcm = (uint32_t*)rt.hcm.p;
       ha.obase = (unsigned long long*)rt.hobase.p;
+      ha.htmn = (uint32_t*)rt.htmn.p;
+      ha.htmx = (uint32_t*)rt.htmx.p;
+      ha.hflag = (uint8_t*)rt.hflag.p;
+      ha.btol = (uint32_t*)rt.btol.p;
       ha.max_blocks = rt.hot_blocks;
       ha.khdr = wa.khdr;
       ha.kslot = wa.kslot;
@@ -2205,7 +2214,8 @@ void cep_destroy(cep_app* a) {
     dev_free(&p.pool_cur);
     for (DevBuf* b : {&p.tkey, &p.tval, &p.krev, &p.kcount, &p.dense}) dev_free(b);
     for (DevBuf* b : {&p.hot_id, &p.hot_key, &p.hot_m, &p.hot_gbase, &p.hoff, &p.cand, &p.ncand, &p.harr, &p.hrow,
-                      &p.hnb, &p.bsum, &p.bcnt, &p.boff, &p.hcm, &p.hobase, &p.hot_active})
+                      &p.hnb, &p.bsum, &p.bcnt, &p.boff, &p.hcm, &p.hobase, &p.hot_active, &p.htmn,
+                      &p.htmx, &p.hflag, &p.btol})
       dev_free(b);
     host_free(&p.hot_active_host);
     if (p.hot_fork) hipEventDestroy(p.hot_fork);

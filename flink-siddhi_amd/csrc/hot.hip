@@ -68,6 +68,23 @@ __device__ __forceinline__ uint32_t hot_total(const HotArgs& a) { return a.hot_g
 
 __device__ __forceinline__ bool within_w(int64_t W, int64_t d) { return W < 0 || (d < 0 ? -d : d) <= W; }
 
+// Order-tolerant records (pat.tolerant, as cf_kernels.hip): role 4 = a
+// B-stream row failing g (expires partials, completes none); record ts are
+// stored as ts - chunk base + 2^31.
+constexpr uint32_t kRolePB = 4;
+constexpr int64_t kTolBias = 1ll << 31;
+constexpr uint32_t kTolEmptyMn = 0xffffffffu, kTolEmptyMx = 0u;   // empty range: mn > mx
+
+__device__ __forceinline__ int64_t hot_ts_base(const HotArgs& a) {
+  return a.chunk_base[0] - (a.pat.tolerant ? kTolBias : 0);
+}
+
+// a partial started at record ts t (record units) survives every B-stream row
+// of the range [mn, mx] (empty: mn > mx)
+__device__ __forceinline__ bool tol_ok(int64_t W, int64_t t, uint32_t mn, uint32_t mx) {
+  return mn > mx || W < 0 || (t - (int64_t)mn <= W && (int64_t)mx - t <= W);
+}
+
 // Arrival number of the record at chunk row r (received shuffle records carry
 // their global number; local rows are numbered from the chunk base).
 __device__ __forceinline__ int64_t row_seq_of(const HotArgs& a, int64_t seq_base, uint32_t r) {
@@ -208,6 +225,7 @@ __global__ __launch_bounds__(kHT) void k_hot_gather(HotArgs a) {
 }
 
 // ---- per block: next B inside the block (segmented suffix scan) -----------
+template <bool TOL>   // TOL: also the order-tolerant ranges (their LDS only in that build)
 __global__ __launch_bounds__(kHT) void k_hot_local(HotArgs a) {
   __shared__ uint16_t sl[kHotBlock];
   __shared__ uint32_t v0[kHotBlock], v1[kHotBlock];
@@ -245,6 +263,127 @@ __global__ __launch_bounds__(kHT) void k_hot_local(HotArgs a) {
     s[0] = sl[0];
     s[1] = cur[0] == kNoPos ? kNoPos : p0 + cur[0];
     s[2] = sl[n - 1];
+  }
+  if constexpr (TOL) {
+    // per record: min / max ts of the B-stream rows from it to the next
+    // g-passing B of its slot inclusive, inside the block (segmented suffix
+    // scan by doubling; open: the range runs into the next block)
+    __shared__ uint32_t tmn[2][kHotBlock], tmx[2][kHotBlock];
+    __shared__ uint8_t top[2][kHotBlock];
+    lds_barrier();
+    for (uint32_t i = threadIdx.x; i < n; i += kHT) {
+      const uint64_t w0 = a.harr[(int64_t)(p0 + i) * RW];
+      const uint32_t role = h_role(w0), t = (uint32_t)w0;
+      const bool bs = (role & (ROLE_B | kRolePB)) != 0;
+      tmn[0][i] = bs ? t : kTolEmptyMn;
+      tmx[0][i] = bs ? t : kTolEmptyMx;
+      top[0][i] = (role & ROLE_B) ? 0 : 1;   // a g-passing B ends the range of the records before it
+    }
+    lds_barrier();
+    int c = 0;
+    for (uint32_t d = 1; d < n; d <<= 1) {
+      for (uint32_t i = threadIdx.x; i < n; i += kHT) {
+        uint32_t mn = tmn[c][i], mx = tmx[c][i];
+        uint8_t o = top[c][i];
+        if (o && i + d < n) {
+          if (sl[i + d] == sl[i]) {
+            const uint32_t m2 = tmn[c][i + d], x2 = tmx[c][i + d];
+            mn = m2 < mn ? m2 : mn;
+            mx = x2 > mx ? x2 : mx;
+            o = top[c][i + d];
+          } else {
+            o = 0;   // the slot ends inside the block
+          }
+        }
+        tmn[c ^ 1][i] = mn;
+        tmx[c ^ 1][i] = mx;
+        top[c ^ 1][i] = o;
+      }
+      lds_barrier();
+      c ^= 1;
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += kHT) {
+      a.htmn[p0 + i] = tmn[c][i];
+      a.htmx[p0 + i] = tmx[c][i];
+      a.hflag[p0 + i] = top[c][i];
+    }
+    if (threadIdx.x == 0) {
+      uint32_t* b = a.btol + (int64_t)blockIdx.x * 3;
+      b[0] = tmn[c][0];
+      b[1] = tmx[c][0];
+      b[2] = top[c][0];
+    }
+  }
+}
+
+// ---- order-tolerant builds, one workgroup: the resolved range of every
+// block's first record (btol[3b], btol[3b + 1]): its own range, continued
+// into the next block's first record's resolved range while open and linked
+// (the next block starts with the same slot).  Chunks of blocks per thread,
+// chunk heads resolved by doubling, then each chunk re-walked.
+__global__ __launch_bounds__(kHT) void k_hot_carry_tol(HotArgs a) {
+  __shared__ uint32_t hm[2][kHT], hx[2][kHT];
+  __shared__ uint8_t ho[2][kHT];
+  const uint32_t M = hot_total(a);
+  const int nb = (int)((M + kHotBlock - 1) / kHotBlock);
+  if (nb == 0) return;
+  const int tid = threadIdx.x;
+  const int cpt = (nb + kHT - 1) / kHT;
+  const int b0 = tid * cpt, b1 = min(nb, b0 + cpt);
+  auto linked = [&](int b) -> bool {
+    return b + 1 < nb && a.bsum[(int64_t)b * 4 + 2] == a.bsum[(int64_t)(b + 1) * 4];
+  };
+  uint32_t mn = kTolEmptyMn, mx = kTolEmptyMx;
+  bool open = b0 < b1;
+  for (int b = b1 - 1; b >= b0; --b) {
+    const uint32_t* t = a.btol + (int64_t)b * 3;
+    if (t[2] && linked(b)) {
+      mn = t[0] < mn ? t[0] : mn;
+      mx = t[1] > mx ? t[1] : mx;
+    } else {
+      mn = t[0];
+      mx = t[1];
+      open = false;
+    }
+  }
+  int c = 0;
+  hm[0][tid] = mn;
+  hx[0][tid] = mx;
+  ho[0][tid] = open ? 1 : 0;
+  lds_barrier();
+  for (int d = 1; d < kHT; d <<= 1) {
+    uint32_t m = hm[c][tid], x = hx[c][tid];
+    uint8_t o = ho[c][tid];
+    if (o) {
+      if (tid + d < kHT) {
+        const uint32_t m2 = hm[c][tid + d], x2 = hx[c][tid + d];
+        m = m2 < m ? m2 : m;
+        x = x2 > x ? x2 : x;
+        o = ho[c][tid + d];
+      } else {
+        o = 0;
+      }
+    }
+    hm[c ^ 1][tid] = m;
+    hx[c ^ 1][tid] = x;
+    ho[c ^ 1][tid] = o;
+    lds_barrier();
+    c ^= 1;
+  }
+  // the resolved range at the next chunk's first block, then this chunk right to left
+  uint32_t rm = tid + 1 < kHT ? hm[c][tid + 1] : kTolEmptyMn;
+  uint32_t rx = tid + 1 < kHT ? hx[c][tid + 1] : kTolEmptyMx;
+  for (int b = b1 - 1; b >= b0; --b) {
+    uint32_t* t = a.btol + (int64_t)b * 3;
+    uint32_t fm = t[0], fx = t[1];
+    if (t[2] && linked(b)) {
+      fm = rm < fm ? rm : fm;
+      fx = rx > fx ? rx : fx;
+    }
+    t[0] = fm;
+    t[1] = fx;
+    rm = fm;
+    rx = fx;
   }
 }
 
@@ -323,12 +462,14 @@ __device__ __forceinline__ uint32_t block_carry(const HotArgs& a, int b, int nb)
 
 __device__ __forceinline__ bool hot_matched(const HotArgs& a, uint32_t p, uint32_t nbv, int RW) {
   if (nbv == kNoPos) return false;
+  if (a.pat.tolerant) return (a.hflag[p] & 2u) != 0;   // an A alive at its next B (k_hot_flags)
   const uint64_t w0 = a.harr[(int64_t)p * RW];
   if (!(h_role(w0) & ROLE_A)) return false;
   const uint64_t wb = a.harr[(int64_t)nbv * RW];
   return within_w(a.pat.within, (int64_t)(uint32_t)wb - (int64_t)(uint32_t)w0);
 }
 
+template <bool TOL>
 __global__ __launch_bounds__(kHT) void k_hot_flags(HotArgs a) {
   __shared__ uint32_t scratch[16];
   const uint32_t M = hot_total(a);
@@ -339,6 +480,47 @@ __global__ __launch_bounds__(kHT) void k_hot_flags(HotArgs a) {
   const int RW = rec_words(a);
   const uint32_t carry = block_carry(a, blockIdx.x, nb);
   const uint32_t last = a.bsum[(int64_t)blockIdx.x * 4 + 2];
+  if constexpr (TOL) {
+    // resolved ranges (open ones continue into the next block's first
+    // record), then each A's flag: alive iff every B-stream row after it up
+    // to its next g-passing B (or the slot end) is within W of it
+    __shared__ uint32_t fm[kHotBlock], fx[kHotBlock];
+    __shared__ uint16_t fs[kHotBlock];
+    const bool lk = blockIdx.x + 1 < nb && a.bsum[(int64_t)(blockIdx.x + 1) * 4] == last;
+    const uint32_t cm = lk ? a.btol[(int64_t)(blockIdx.x + 1) * 3] : kTolEmptyMn;
+    const uint32_t cx = lk ? a.btol[(int64_t)(blockIdx.x + 1) * 3 + 1] : kTolEmptyMx;
+    for (uint32_t i = threadIdx.x; i < n; i += kHT) {
+      const uint32_t p = p0 + i;
+      uint32_t mn = a.htmn[p], mx = a.htmx[p];
+      if ((a.hflag[p] & 1u) && lk) {
+        mn = cm < mn ? cm : mn;
+        mx = cx > mx ? cx : mx;
+      }
+      fm[i] = mn;
+      fx[i] = mx;
+      fs[i] = (uint16_t)h_slot(a.harr[(int64_t)p * RW]);
+      a.htmn[p] = mn;
+      a.htmx[p] = mx;
+    }
+    lds_barrier();
+    for (uint32_t i = threadIdx.x; i < n; i += kHT) {
+      const uint32_t p = p0 + i;
+      const uint64_t w0 = a.harr[(int64_t)p * RW];
+      uint32_t mn = kTolEmptyMn, mx = kTolEmptyMx;   // the range after this record
+      if (i + 1 < n) {
+        if (fs[i + 1] == fs[i]) {
+          mn = fm[i + 1];
+          mx = fx[i + 1];
+        }
+      } else if (lk) {
+        mn = cm;
+        mx = cx;
+      }
+      const bool alive = (h_role(w0) & ROLE_A) && tol_ok(a.pat.within, (int64_t)(uint32_t)w0, mn, mx);
+      a.hflag[p] = (uint8_t)((a.hflag[p] & 1u) | (alive ? 2u : 0u));
+    }
+    __threadfence_block();
+  }
   uint32_t c = 0;
   for (uint32_t i = threadIdx.x; i < n; i += kHT) {
     const uint32_t p = p0 + i;
@@ -392,7 +574,16 @@ __global__ __launch_bounds__(kHT) void k_hot_offsets(HotArgs a) {
       const int n = ovf ? (int)(uint32_t)ext : (int)(hdr & 0xffu);
       const uint32_t g = a.hot_gbase[h];
       const uint32_t fb = (h_role(a.harr[(int64_t)g * RW]) & ROLE_B) ? g : a.hnb[g];
-      if (n > 0 && fb != kNoPos) {
+      if (a.pat.tolerant) {
+        // carried partials alive at the first g-passing B: the B-stream rows
+        // from the slot start to it inclusive (the resolved range of record g)
+        if (n > 0 && fb != kNoPos) {
+          const int64_t tb = hot_ts_base(a);
+          const uint32_t mn = a.htmn[g], mx = a.htmx[g];
+          for (int j = 0; j < n; ++j)
+            cm += tol_ok(a.pat.within, (int64_t)slot_word(a, kidx, j, 0, ext >> 32) - tb, mn, mx) ? 1u : 0u;
+        }
+      } else if (n > 0 && fb != kNoPos) {
         const int64_t tb = a.chunk_base[0] + (int64_t)(uint32_t)a.harr[(int64_t)fb * RW];
         int j = 0;
         while (j < n && !within_w(a.pat.within, tb - (int64_t)slot_word(a, kidx, j, 0, ext >> 32))) ++j;
@@ -432,7 +623,7 @@ __global__ __launch_bounds__(kHT) void k_hot_emit(HotArgs a) {
   // rounds of kHT consecutive records (lane-interleaved): each round's rows
   // are consecutive positions, so the column stores coalesce
   unsigned long long base = a.obase[0] + a.obase[1] + a.boff[blockIdx.x];
-  const int64_t ts_base = a.chunk_base[0], seq_base = a.chunk_base[1];
+  const int64_t ts_base = hot_ts_base(a), seq_base = a.chunk_base[1];
   for (uint32_t r0 = 0; r0 < n; r0 += kHT) {
     const uint32_t i = r0 + threadIdx.x;
     const uint32_t p = p0 + i;
@@ -472,7 +663,8 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
   const uint64_t ovoff = ext >> 32;
   const int n = ovf ? (int)(uint32_t)ext : (int)(hdr & 0xffu);
   const uint32_t m = a.hot_m[h];
-  const int64_t ts_base = a.chunk_base[0], seq_base = a.chunk_base[1];
+  const bool tol = a.pat.tolerant != 0;
+  const int64_t ts_base = hot_ts_base(a), seq_base = a.chunk_base[1];
   const int cp0 = a.cf.cap_phys[0], cp1 = a.cf.cap_phys[1];
   (void)cp0;
   (void)cp1;
@@ -522,11 +714,32 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
     if (lb == kNoPos && bb) lb = (uint32_t)(base - (__ffsll((long long)bb) - 1));
     if (la == kNoPos && ba) la = (uint32_t)(base - (__ffsll((long long)ba) - 1));
   }
-  const bool prune = W >= 0 && la != kNoPos;
+  const bool prune = !tol && W >= 0 && la != kNoPos;   // (tol: no pruning at A arrivals)
+  // tol: the slot's first range (B-stream rows up to its first g-passing B)
+  const uint32_t tmn0 = tol ? a.htmn[g] : 0u, tmx0 = tol ? a.htmx[g] : 0u;
+  auto carried_alive = [&](int j) {
+    return tol_ok(W, (int64_t)slot_word(a, kidx, j, 0, ovoff) - ts_base, tmn0, tmx0);
+  };
   const int64_t last_a_ts = la != kNoPos ? ts_base + (int64_t)(uint32_t)a.harr[(int64_t)la * RW] : 0;
   // carried rows completed by the first B
   const uint32_t cm = a.hcm[h * 3 + 0], cfirst = a.hcm[h * 3 + 1], cm_off = a.hcm[h * 3 + 2];
-  if (cm) {
+  if (cm && tol) {
+    // the carried partials alive at the first B, in slot order
+    const uint64_t* rb = a.harr + (int64_t)fb * RW;
+    const int64_t bts = ts_base + (int64_t)(uint32_t)rb[0];
+    const uint64_t b0 = a.cf.nw > 0 ? rb[1] : 0ull, b1 = a.cf.nw > 1 ? rb[2] : 0ull;
+    uint32_t o = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      const bool al = j < n && carried_alive(j);
+      const unsigned long long bal = __ballot(al);
+      if (al)
+        hot_emit_row(a, a.obase[0] + cm_off + o + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), kf,
+                     c1 ? slot_word(a, kidx, j, 2, ovoff) : 0ull, c2 ? slot_word(a, kidx, j, 3, ovoff) : 0ull,
+                     b0, b1, bts, row_seq_of(a, seq_base, a.hrow[fb]));
+      o += (uint32_t)__popcll(bal);
+    }
+  } else if (cm) {
     const uint64_t* rb = a.harr + (int64_t)fb * RW;
     const int64_t bts = ts_base + (int64_t)(uint32_t)rb[0];
     const uint64_t b0 = a.cf.nw > 0 ? rb[1] : 0ull, b1 = a.cf.nw > 1 ? rb[2] : 0ull;
@@ -540,10 +753,20 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
   // every A from the last B on (a record that is both B and A starts a new
   // partial after completing the others) minus pruned ones
   int drop = 0;
-  if (lb == kNoPos) {
-    while (drop < n && prune && last_a_ts - (int64_t)slot_word(a, kidx, drop, 0, ovoff) > W) ++drop;
+  int keep = 0;
+  if (tol) {
+    // (no B) the carried partials that survive the slot's B-stream rows
+    if (lb == kNoPos)
+      for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        keep += __popcll(__ballot(j < n && carried_alive(j)));
+      }
+  } else {
+    if (lb == kNoPos) {
+      while (drop < n && prune && last_a_ts - (int64_t)slot_word(a, kidx, drop, 0, ovoff) > W) ++drop;
+    }
+    keep = lb == kNoPos ? n - drop : 0;
   }
-  const int keep = lb == kNoPos ? n - drop : 0;
   const uint32_t from = lb == kNoPos ? g : lb;
   // count the new partials (wave ballots), then allocate the overflow run
   int nnew = 0;
@@ -552,7 +775,8 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
     bool take = false;
     if (p < e) {
       const uint64_t w0 = a.harr[(int64_t)p * RW];
-      take = (h_role(w0) & ROLE_A) && !(prune && last_a_ts - (ts_base + (int64_t)(uint32_t)w0) > W);
+      take = (h_role(w0) & ROLE_A) && !(prune && last_a_ts - (ts_base + (int64_t)(uint32_t)w0) > W) &&
+             (!tol || (a.hflag[p] & 2u));
     }
     nnew += __popcll(__ballot(take));
   }
@@ -569,8 +793,27 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
     nov = off;
   }
   // kept carried partials: slot j <- old slot j + drop (all lanes read a
-  // round's old slots before any lane writes: one wave, loads before stores)
-  for (int j0 = 0; j0 < keep; j0 += 64) {
+  // round's old slots before any lane writes: one wave, loads before stores);
+  // tol: the alive ones compacted (a write never passes the slot it read)
+  if (tol && keep > 0) {
+    int w = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      uint64_t ts = 0, x0 = 0, x1 = 0;
+      bool al = false;
+      if (j < n) {
+        ts = slot_word(a, kidx, j, 0, ovoff);
+        x0 = c1 ? slot_word(a, kidx, j, 2, ovoff) : 0ull;
+        x1 = c2 ? slot_word(a, kidx, j, 3, ovoff) : 0ull;
+        al = tol_ok(W, (int64_t)ts - ts_base, tmn0, tmx0);
+      }
+      const unsigned long long bal = __ballot(al);
+      __builtin_amdgcn_wave_barrier();
+      if (al) put(w + __popcll(bal & ((1ull << lane) - 1ull)), ts, x0, x1, nov);
+      w += __popcll(bal);
+    }
+  }
+  for (int j0 = 0; j0 < (tol ? 0 : keep); j0 += 64) {
     const int j = j0 + lane;
     uint64_t ts = 0, x0 = 0, x1 = 0;
     if (j < keep) {
@@ -588,7 +831,8 @@ __global__ __launch_bounds__(64) void k_hot_commit(HotArgs a) {
     uint64_t w0 = 0;
     if (p < e) {
       w0 = a.harr[(int64_t)p * RW];
-      take = (h_role(w0) & ROLE_A) && !(prune && last_a_ts - (ts_base + (int64_t)(uint32_t)w0) > W);
+      take = (h_role(w0) & ROLE_A) && !(prune && last_a_ts - (ts_base + (int64_t)(uint32_t)w0) > W) &&
+             (!tol || (a.hflag[p] & 2u));
     }
     const unsigned long long bal = __ballot(take);
     if (take) {
@@ -755,9 +999,16 @@ void launch_hot_match(const HotArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_hot_count, dim3(kCfHotMax), dim3(kHT), 0, s, a);
   hipLaunchKernelGGL(k_hot_base, dim3(1), dim3(kHT), 0, s, a);
   hipLaunchKernelGGL(k_hot_gather, dim3((unsigned)a.ntiles), dim3(kHT), 0, s, a);
-  hipLaunchKernelGGL(k_hot_local, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
+  const bool tol = a.pat.tolerant != 0;
+  if (tol) hipLaunchKernelGGL(k_hot_local<true>, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
+  else hipLaunchKernelGGL(k_hot_local<false>, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
   hipLaunchKernelGGL(k_hot_carry, dim3(1), dim3(kHT), 0, s, a);
-  hipLaunchKernelGGL(k_hot_flags, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
+  if (tol) {
+    hipLaunchKernelGGL(k_hot_carry_tol, dim3(1), dim3(kHT), 0, s, a);
+    hipLaunchKernelGGL(k_hot_flags<true>, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_hot_flags<false>, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
+  }
   hipLaunchKernelGGL(k_hot_offsets, dim3(1), dim3(kHT), 0, s, a);
   hipLaunchKernelGGL(k_hot_emit, dim3((unsigned)a.max_blocks), dim3(kHT), 0, s, a);
   hipLaunchKernelGGL(k_hot_commit, dim3(kCfHotMax), dim3(64), 0, s, a);

@@ -376,6 +376,15 @@ struct HotArgs {
   uint32_t* bcnt;              // per block: record matches
   uint32_t* boff;
   uint32_t* hcm;               // per slot: carried partials completed, first completed index
+  // order-tolerant builds (pat.tolerant): per hot record the ts range
+  // [htmn, htmx] (record ts units) of the B-stream rows from it to its slot's
+  // next g-passing B inclusive (empty: htmn > htmx); hflag bit 0 = that range
+  // still open at the block end, bit 1 = an A that survives to its next B /
+  // the slot end; per block its first record's range [mn, mx, open] (btol)
+  uint32_t* htmn;
+  uint32_t* htmx;
+  uint8_t* hflag;
+  uint32_t* btol;
   unsigned long long* obase;   // [0]: output base, [1]: carried rows total
   int32_t max_blocks;
   uint32_t* khdr;

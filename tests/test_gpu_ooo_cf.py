@@ -124,3 +124,28 @@ def test_tolerant_then_ordered_state_carries():
     order = np.concatenate([np.arange(third), np.arange(2 * third - 1, third - 1, -1), np.arange(2 * third, n)])
     w = {c: np.ascontiguousarray(w[c][order]) for c in COLS}
     check(w, [third, third, n - 2 * third], keys, chunk=1 << 20)
+
+
+def zipf_disorder_case(n, keys, rate, jitter, seed, chunk=1 << 25):
+    w = CO.generate(0, n, keys, rate=rate, threads=16)
+    w["k"] = np.ascontiguousarray(workload.zipf_map(keys)[w["k"]].astype(np.int32))
+    w = disorder(w, jitter, seed)
+    out, st = run_engine(w, [n // 2 + 17, n - n // 2 - 17], keys, chunk)
+    assert st.hot_keys > 0          # the hot-key kernels ran (their order-tolerant scans)
+    want = oracle_rows(w, keys)
+    assert st.matches_out == len(want["k"])
+    assert_same_per_key(out, want)
+    return len(want["k"])
+
+
+def test_zipf_keys_with_disorder_vs_oracle():
+    # Zipf s = 1.1 over the bench's 2^20 keys: the hottest keys go through
+    # hot.hip, whose scans carry the B-stream ts ranges across 2048-record
+    # blocks; disorder of up to 2 M arrivals (5 s of stream time at 400/ms)
+    assert zipf_disorder_case(1 << 24, 1 << 20, 400, 2_000_000, seed=5) > 500_000
+
+
+def test_zipf_keys_dense_rate_disorder_vs_oracle():
+    # few keys, 20 events per ms: hot keys span many blocks and keep long
+    # lists (pool); jitter of 100 k arrivals = 5 s against W = 10 s
+    assert zipf_disorder_case(1 << 22, 1 << 16, 20, 100_000, seed=9, chunk=1 << 22) > 50_000
