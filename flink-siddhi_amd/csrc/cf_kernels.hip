@@ -883,7 +883,9 @@ __global__ __launch_bounds__(kCfWalkThreads, 4) void k_cfwalk(CfWalkArgs a) {   
         const uint64_t w0 = ((uint64_t)x[i].y << 32) | x[i].x;
         L.sts[s] = x[i].x;
         L.sseq[s] = hs[i];
-        if (a.in_seq)   // received records: global arrival number - chunk base
+        // received records: global arrival number - chunk base (read only
+        // when the output stores seq: a scattered load per record)
+        if (a.in_seq && a.out.write_seq)
           L.sseq[s] = (uint32_t)((int64_t)a.in_seq[(int64_t)hs[i] * a.in_rec_words] - seq_base);
         L.skr[s] = (uint16_t)(rec_key(w0) | (rec_role(w0) << 12));
         if (NW > 0) L.scap[0][s] = ((uint64_t)x[i].w << 32) | x[i].z;

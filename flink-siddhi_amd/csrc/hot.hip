@@ -88,7 +88,8 @@ __device__ __forceinline__ bool tol_ok(int64_t W, int64_t t, uint32_t mn, uint32
 // Arrival number of the record at chunk row r (received shuffle records carry
 // their global number; local rows are numbered from the chunk base).
 __device__ __forceinline__ int64_t row_seq_of(const HotArgs& a, int64_t seq_base, uint32_t r) {
-  return a.in_seq ? (int64_t)a.in_seq[(int64_t)r * a.in_rec_words] : seq_base + (int64_t)r;
+  // (output seq not stored: not read)
+  return (a.in_seq && a.out.write_seq) ? (int64_t)a.in_seq[(int64_t)r * a.in_rec_words] : seq_base + (int64_t)r;
 }
 
 // One output row (as k_cfwalk's cf_emit).
