@@ -114,7 +114,11 @@ __device__ __forceinline__ uint32_t rec_key(uint64_t w0) { return (uint32_t)(w0 
 template <int NW, bool FR, int NP = kPref, bool TOL = false>
 __global__ __launch_bounds__(kCfPartThreads, CF_PART_MINW) void k_cfpart(CfPartArgs a) {
   constexpr int E = kCfItems, NT = kCfPartThreads, RW = 1 + NW;
-  constexpr int kStageRecs = kCfStageBytes / (8 * RW);
+  // received records (FR: every row is kept) and order-tolerant tiles (~3/4
+  // kept) need a larger stage to store their tile as one coalesced run; the
+  // kernel runs one workgroup per CU either way (128 VGPRs x 1024 lanes)
+  constexpr int kStageBytesT = (FR || TOL) ? 128 * 1024 : kCfStageBytes;
+  constexpr int kStageRecs = kStageBytesT / (8 * RW);
   __shared__ uint32_t scratch[NT / 64 + 1];
   __shared__ __attribute__((aligned(16))) uint64_t stage[kStageRecs * RW];
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // NB + 1 (dynamic)
