@@ -125,11 +125,14 @@ typedef struct cep_options {
                               a partial waits on is kept, and a partial is dropped exactly
                               when SURVEY App. A.3 drops it (|ts(event) - ts(s1)| > W, on
                               events of that stream), so the state and every match equal the
-                              oracle's for any order.
+                              oracle's for any order.  `every A -> B` patterns take the
+                              closed form's order-tolerant build (hot keys included; a
+                              chunk's ts must lie within +-2^31 ms of its first row's, else
+                              the flush fails with CEP_E_ARG), other shapes the N-state walk.
                               1: the caller guarantees non-decreasing ts (event-time order,
                               e.g. a watermark drain with late_policy 0): the event-time fast
                               paths (closed form, predicate push-down of B's, pruning at A
-                              arrivals, hot keys), several times faster; a descent fails the
+                              arrivals, hot keys), ~2x faster on config 3; a descent fails the
                               next cep_flush with CEP_E_ARG.  Sequences and multi-query groups
                               prune by |ts - ts(s1)| in any order either way (ts_order 1
                               only adds the check); the multi-GPU record / row shuffles
